@@ -1,0 +1,154 @@
+"""ctypes binding of ``libcfa.so`` (the C-ABI declared in ``include/cfa_engine.h``).
+
+This is the thin shim between the Python consensus surface and the HIP kernels. There is no
+fallback: if the library is missing or cannot be loaded, every compute entry point raises.
+
+The library links against ``libamdhip64.so.7``/``librccl.so.1`` by soname. PyTorch-ROCm ships
+its own copies of those libraries; importing torch first makes the dynamic loader bind
+libcfa to the very same HIP runtime torch uses (same soname => same loaded object), so device
+pointers and hipStream_t handles from torch tensors/streams are valid in libcfa.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- must be loaded before libcfa (see module docstring)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.environ.get("CFA_LIB", os.path.join(LIB_DIR, "libcfa.so"))
+
+CFA_OK = 0
+CFA_E_INVALID = -1
+CFA_E_HIP = -2
+CFA_E_RCCL = -3
+CFA_E_UNSUPPORTED = -4
+
+CFA_MAX_FANIN = 16
+CFA_UNIQUE_ID_BYTES = 128
+
+RULE_SEQUENTIAL = 0
+RULE_LINEAR = 1
+
+COMPRESS_NONE = 0
+COMPRESS_SPARSE = 1
+COMPRESS_SPARSE_DPCM = 2
+COMPRESS_SPARSE_DPCM_HI = 3
+COMPRESS_SPARSE_HI = 4
+
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_c_void_p = ctypes.c_void_p
+_c_size_t = ctypes.c_size_t
+_c_int = ctypes.c_int
+_c_int64_p = ctypes.POINTER(ctypes.c_int64)
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_PP = ctypes.POINTER(ctypes.c_void_p)  # float* const* (host table of device pointers)
+
+# name -> (restype, argtypes); mirrors include/cfa_engine.h one for one.
+SIGNATURES = {
+    "cfa_version": (_c_int, []),
+    "cfa_last_error": (ctypes.c_char_p, []),
+    "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
+    "cfa_mix_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
+    "cfa_mix_strided_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_int64_p, _c_float_p, _c_int,
+                                     _c_size_t, _c_void_p]),
+    "cfa_mix_seq_compress_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
+                                          _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_compress_epilogue_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p,
+                                           _c_void_p]),
+    "cfa_mewma_update_f32": (_c_int, [_c_void_p, _PP, _PP, _c_int64_p, _c_int, ctypes.c_double,
+                                      ctypes.c_float, ctypes.c_float, _c_size_t, _c_int, _c_int,
+                                      _c_size_t, _c_void_p]),
+    "cfa_mix_population_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_int, _c_int, _c_size_t, _c_void_p]),
+    "cfa_comm_unique_id": (_c_int, [_c_void_p]),
+    "cfa_comm_init": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_void_p, _c_int]),
+    "cfa_comm_destroy": (_c_int, [_c_void_p]),
+    "cfa_halo_exchange_f32": (_c_int, [_c_void_p, _PP, _c_int_p, _c_int, _PP, _c_int_p, _c_int,
+                                       _c_size_t, _c_void_p]),
+    "cfa_allreduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
+    "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class CFAError(RuntimeError):
+    """A libcfa call returned a negative status."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed with code {code}: {msg}")
+        self.code = code
+
+
+def load() -> ctypes.CDLL:
+    """Load libcfa.so once (thread-safe) and bind every C-ABI signature. Raises if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.isfile(LIB_PATH):
+                raise ImportError(
+                    f"libcfa.so not found at {LIB_PATH}; build it with "
+                    "`make -C federated_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a C-ABI entry point; raise CFAError with the library's message on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != CFA_OK:
+        msg = lib.cfa_last_error()
+        raise CFAError(name, rc, msg.decode() if msg else "")
+
+
+def ptr_table(ptrs) -> "ctypes.Array":
+    """Host array of device pointers (ints) for the `float* const*` arguments."""
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def float_array(vals) -> "ctypes.Array":
+    arr = (ctypes.c_float * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def int64_array(vals) -> "ctypes.Array":
+    arr = (ctypes.c_int64 * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def int_array(vals) -> "ctypes.Array":
+    arr = (ctypes.c_int * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def loaded_hip_runtimes() -> list:
+    """Paths of every libamdhip64 mapped into this process (must be exactly one)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                if "libamdhip64" in line:
+                    paths.add(line.split()[-1])
+    except OSError:
+        pass
+    return sorted(paths)

@@ -1,0 +1,816 @@
+// cfa_engine.hip — gfx950 (MI355X / CDNA4) kernels + C-ABI for CFA / CFA-GE consensus mixing.
+//
+// The reference computes the mixing step as numpy AXPY chains over whole tensors, one
+// neighbour at a time, with a file round trip between neighbours:
+//   TF1/consensus/cfa.py:66-76, cfa_ongraphs.py:109-119, cfa_ge_2stage.py:73-83 / 594-621,
+//   TF2 consensus_v3.py:153-155, consensus_v4.py:211-213 / 251-253.
+// Here one launch folds every neighbour of a device in registers: each lane streams one
+// 16-byte slice of the local bucket and of all n neighbour buckets from HBM, applies the
+// rule, and writes the result once. The work is HBM-bound (0.2-0.45 flop/byte), so there is
+// no MFMA and no LDS data staging: the mixing coefficients and the bucket pointers live in
+// the kernel arguments (SGPRs), loads are 16 B/lane (global_load_dwordx4), every load of a
+// tile is issued before the first use, and the fan-in N is a template parameter so the
+// fold is fully unrolled.
+//
+// Numerics: this file is compiled with -ffp-contract=off. CFA_RULE_SEQUENTIAL evaluates
+// t = x - w; t = a * t; w = w + t exactly as fp32 numpy does (three roundings), which makes
+// the TF2 path bit-identical to the reference. CFA_RULE_LINEAR uses explicit fmaf.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "cfa_engine.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// Error reporting (thread-local, no global mutable state shared between threads).
+// ------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define CFA_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(CFA_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                  __FILE__, __LINE__);                                                   \
+  } while (0)
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CFA_E_HIP, "%s launch failed: %s", what, hipGetErrorString(e));
+  return CFA_OK;
+}
+
+extern "C" int cfa_version(void) { return CFA_VERSION; }
+extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }
+// Used by cfa_comm.cpp so both translation units report through one thread-local message.
+extern "C" __attribute__((visibility("hidden"))) void cfa_internal_set_error(const char* msg) {
+  g_last_error = msg ? msg : "";
+}
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// Launch tuning, read once from the environment (immutable after first use).
+struct Tune {
+  int blocks_per_cu;  // grid = min(tiles, CUs * blocks_per_cu); 0 = one block per tile
+  int unroll;         // 16-byte vectors per lane per stream per tile (1 or 2)
+  int nontemporal;    // 1 = nontemporal loads/stores for the once-read streams
+};
+
+static Tune read_tune() {
+  Tune t{0, 2, 1};
+  if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
+  if (const char* s = getenv("CFA_UNROLL")) t.unroll = atoi(s) >= 2 ? 2 : 1;
+  if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
+  return t;
+}
+static const Tune& tune() {
+  static const Tune t = read_tune();  // C++11 magic static: thread-safe init
+  return t;
+}
+
+static int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 256;
+  return cus;
+}
+
+static unsigned grid_for(long long tiles) {
+  if (tiles <= 0) return 1;
+  const Tune& t = tune();
+  long long g = tiles;
+  if (t.blocks_per_cu > 0) {
+    long long cap = (long long)device_cus() * t.blocks_per_cu;
+    if (g > cap) g = cap;
+  }
+  if (g > 0x7fffffffLL) g = 0x7fffffffLL;
+  return (unsigned)g;
+}
+
+// Kernel-argument pack: pointers + coefficients land in SGPRs.
+struct Fanin {
+  const float* src[CFA_MAX_FANIN + 1];  // [0] = local (w0), [1..N] = neighbours
+  float c[CFA_MAX_FANIN + 1];           // SEQ: c[j] = alpha of src[j] (c[0] unused); LIN: coeff
+};
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float* p, long long i) {
+  const f4* q = reinterpret_cast<const f4*>(p) + i;
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, long long i, f4 v) {
+  f4* q = reinterpret_cast<f4*>(p) + i;
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
+template <int N, int RULE>
+__device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
+  if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+    f4 w = v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      f4 t = v[j] - w;  // numpy: (x - w)
+      t = f.c[j] * t;   //        eps * (...)
+      w = w + t;        //        w + (...)
+    }
+    return w;
+  } else {
+    f4 w = f.c[0] * v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      w.x = fmaf(f.c[j], v[j].x, w.x);
+      w.y = fmaf(f.c[j], v[j].y, w.y);
+      w.z = fmaf(f.c[j], v[j].z, w.z);
+      w.w = fmaf(f.c[j], v[j].w, w.w);
+    }
+    return w;
+  }
+}
+
+// Compression epilogue on one element (TF1/consensus/cfa_ongraphs.py:225-273). The test and
+// the replacement are evaluated in double, as the reference does on its fp64 arrays, then
+// rounded once to fp32. sign(0) = 0 and sign(NaN) = NaN as numpy.
+__device__ __forceinline__ double np_sign(double x) {
+  return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : x);
+}
+struct CompressParams {
+  int mode;
+  double thr, rep;
+  long long cbegin, cend;  // element range the epilogue applies to
+  unsigned long long* kept;
+};
+__device__ __forceinline__ float compress_one(float y, float ref, const CompressParams& cp,
+                                              unsigned& kept) {
+  if (cp.mode == CFA_COMPRESS_SPARSE || cp.mode == CFA_COMPRESS_SPARSE_HI) {
+    const double yd = (double)y;
+    if (fabs(yd) < cp.thr) return (float)(np_sign(yd) * cp.rep);
+  } else if (cp.mode == CFA_COMPRESS_SPARSE_DPCM || cp.mode == CFA_COMPRESS_SPARSE_DPCM_HI) {
+    const double d = (double)y - (double)ref;
+    if (fabs(d) < cp.thr) return (float)((double)ref + np_sign(d) * cp.rep);
+  }
+  ++kept;
+  return y;
+}
+
+// Block-wide sum of one counter per lane, then a single 64-bit atomic per block.
+__device__ __forceinline__ void block_add_count(unsigned kept, unsigned long long* dst) {
+  __shared__ unsigned red[kBlock / 64];
+  unsigned v = kept;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; ++i) s += red[i];
+    if (s) atomicAdd(dst, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Vector mix kernel: tiles of kBlock*U float4 per block, grid-stride over tiles; the last
+// partial tile is handled with per-vector guards by the block that owns it.
+// ------------------------------------------------------------------------------------------
+template <int N, int RULE, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, long long nvec) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<NT>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st4<NT>(out, base + (long long)u * kBlock, fold<N, RULE>(v[u], f));
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+      st4<false>(out, i, fold<N, RULE>(v, f));
+    }
+  }
+}
+
+// Vector mix + fused compression epilogue (count reduction per block).
+template <int N>
+__global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fanin f,
+                                                                   long long nvec,
+                                                                   CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (long long)gridDim.x * kBlock) {
+    f4 v[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+    f4 w = fold<N, CFA_RULE_SEQUENTIAL>(v, f);
+    const long long e0 = i * 4;
+    if (e0 + 3 >= cp.cbegin && e0 < cp.cend) {
+      const f4 r = v[0];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const long long e = e0 + c;
+        if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
+      }
+    }
+    st4<false>(out, i, w);
+  }
+  block_add_count(kept, cp.kept);
+}
+
+// Scalar path: unaligned buckets, the <4-element tail, and strided neighbours.
+struct ScalarFanin {
+  const float* src[CFA_MAX_FANIN + 1];
+  long long stride[CFA_MAX_FANIN + 1];
+  float c[CFA_MAX_FANIN + 1];
+  int n;
+};
+__global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFanin f, long long P,
+                                                            int rule, int compress,
+                                                            CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    const float w0 = f.src[0][i * f.stride[0]];
+    float w;
+    if (rule == CFA_RULE_SEQUENTIAL) {
+      w = w0;
+      for (int j = 1; j <= f.n; ++j) {
+        float t = f.src[j][i * f.stride[j]] - w;
+        t = f.c[j] * t;
+        w = w + t;
+      }
+    } else {
+      w = f.c[0] * w0;
+      for (int j = 1; j <= f.n; ++j) w = fmaf(f.c[j], f.src[j][i * f.stride[j]], w);
+    }
+    if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one(w, w0, cp, kept);
+    out[i] = w;
+  }
+  if (compress) block_add_count(kept, cp.kept);
+}
+
+// Standalone compression epilogue (no mixing): y in place.
+__global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float* ref, long long P,
+                                                          CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    const float r = ref ? ref[i] : 0.0f;
+    y[i] = compress_one(y[i], r, cp, kept);
+  }
+  block_add_count(kept, cp.kept);
+}
+
+// ------------------------------------------------------------------------------------------
+// CFA-GE MEWMA update (TF1/consensus/cfa_ge_2stage.py:593-621, :329-371).
+// ------------------------------------------------------------------------------------------
+struct MewmaArgs {
+  float* W;
+  float* s[CFA_MAX_FANIN];
+  const float* g[CFA_MAX_FANIN];
+  long long gstride[CFA_MAX_FANIN];
+  int n;
+  float rho, one_minus_rho, lr1, lr2;
+  long long split;
+  int init, filtered;
+};
+
+// Contiguous case: float4 per lane, g and s streamed once each.
+__global__ __launch_bounds__(kBlock) void mewma_vec_kernel(MewmaArgs a, long long nvec) {
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (long long)gridDim.x * kBlock) {
+    f4 W = ld4<false>(a.W, i);
+    const long long e0 = i * 4;
+    f4 lr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lr[c] = (e0 + c) < a.split ? a.lr1 : a.lr2;
+    for (int j = 0; j < a.n; ++j) {
+      const f4 g = ld4<false>(a.g[j], i);
+      f4 s;
+      if (a.init) {
+        s = g;
+      } else {
+        const f4 s_old = ld4<false>(a.s[j], i);
+        s = a.rho * g + a.one_minus_rho * s_old;  // numpy: rho*g + (1-rho)*s
+      }
+      st4<false>(a.s[j], i, s);
+      W = W - lr * (a.filtered ? s : g);
+    }
+    st4<false>(a.W, i, W);
+  }
+}
+
+// Generic case: scalar, arbitrary element stride on the gradient buckets.
+__global__ __launch_bounds__(kBlock) void mewma_scalar_kernel(MewmaArgs a, long long begin,
+                                                              long long P) {
+  for (long long i = begin + (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    float W = a.W[i];
+    const float lr = i < a.split ? a.lr1 : a.lr2;
+    for (int j = 0; j < a.n; ++j) {
+      const float g = a.g[j][i * a.gstride[j]];
+      float s;
+      if (a.init) {
+        s = g;
+      } else {
+        float t1 = a.rho * g;
+        float t2 = a.one_minus_rho * a.s[j][i];
+        s = t1 + t2;
+      }
+      a.s[j][i] = s;
+      float u = lr * (a.filtered ? s : g);
+      W = W - u;
+    }
+    a.W[i] = W;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Population round: grid.y = device, grid.x = tiles. CSR lists each device's sources.
+// ------------------------------------------------------------------------------------------
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void population_kernel(float* const* out_ptrs,
+                                                            const float* const* src_ptrs,
+                                                            const int32_t* csr_ptr,
+                                                            const int32_t* csr_idx,
+                                                            const float* csr_coef,
+                                                            long long nvec) {
+  const int d = blockIdx.y;
+  const int e0 = csr_ptr[d];
+  const int e1 = csr_ptr[d + 1];
+  float* out = out_ptrs[d];
+  constexpr int U = 2;
+  constexpr long long kTile = (long long)kBlock * U;
+  for (long long t = blockIdx.x; t * kTile < nvec; t += gridDim.x) {
+    long long idx[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      idx[u] = t * kTile + (long long)u * kBlock + threadIdx.x;
+      ok[u] = idx[u] < nvec;
+    }
+    f4 w[U];
+    const float* s0 = src_ptrs[csr_idx[e0]];
+    const float c0 = csr_coef[e0];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      w[u] = ok[u] ? ld4<true>(s0, idx[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (RULE == CFA_RULE_LINEAR) w[u] = c0 * w[u];
+    }
+    for (int e = e0 + 1; e < e1; ++e) {
+      const float* s = src_ptrs[csr_idx[e]];
+      const float c = csr_coef[e];
+      f4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ok[u] ? ld4<true>(s, idx[u]) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+          f4 tt = x[u] - w[u];
+          tt = c * tt;
+          w[u] = w[u] + tt;
+        } else {
+          w[u].x = fmaf(c, x[u].x, w[u].x);
+          w[u].y = fmaf(c, x[u].y, w[u].y);
+          w[u].z = fmaf(c, x[u].z, w[u].z);
+          w[u].w = fmaf(c, x[u].w, w[u].w);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (ok[u]) st4<true>(out, idx[u], w[u]);
+  }
+}
+
+// Scalar tail for the population kernel (elements [begin, P)).
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void population_tail_kernel(
+    float* const* out_ptrs, const float* const* src_ptrs, const int32_t* csr_ptr,
+    const int32_t* csr_idx, const float* csr_coef, long long begin, long long P) {
+  const int d = blockIdx.y;
+  const long long i = begin + threadIdx.x;
+  if (i >= P) return;
+  const int e0 = csr_ptr[d], e1 = csr_ptr[d + 1];
+  float w = src_ptrs[csr_idx[e0]][i];
+  if constexpr (RULE == CFA_RULE_LINEAR) w = csr_coef[e0] * w;
+  for (int e = e0 + 1; e < e1; ++e) {
+    const float x = src_ptrs[csr_idx[e]][i];
+    const float c = csr_coef[e];
+    if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+      float tt = x - w;
+      tt = c * tt;
+      w = w + tt;
+    } else {
+      w = fmaf(c, x, w);
+    }
+  }
+  out_ptrs[d][i] = w;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-side dispatch.
+// ------------------------------------------------------------------------------------------
+template <int RULE, int U, bool NT>
+static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const Fanin& f,
+                         long long nvec) {
+#define CFA_CASE(K) \
+  case K:           \
+    mix_vec_kernel<K, RULE, U, NT><<<grid, kBlock, 0, st>>>(out, f, nvec); \
+    break;
+  switch (n) {
+    CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
+    CFA_CASE(7) CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13)
+    CFA_CASE(14) CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
+template <int RULE>
+static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec) {
+  const Tune& t = tune();
+  const int U = t.unroll;
+  const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
+  const unsigned grid = grid_for(tiles);
+  if (U == 2) {
+    if (t.nontemporal) launch_vec_u<RULE, 2, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 2, false>(n, grid, st, out, f, nvec);
+  } else {
+    if (t.nontemporal) launch_vec_u<RULE, 1, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 1, false>(n, grid, st, out, f, nvec);
+  }
+}
+
+static void launch_vec_compress(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                                const CompressParams& cp) {
+  const unsigned grid = grid_for((nvec + kBlock - 1) / kBlock);
+#define CFA_CASE(K) \
+  case K:           \
+    mix_vec_compress_kernel<K><<<grid, kBlock, 0, st>>>(out, f, nvec, cp); \
+    break;
+  switch (n) {
+    CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
+    CFA_CASE(7) CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13)
+    CFA_CASE(14) CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
+static inline uintptr_t addr(const void* p) { return reinterpret_cast<uintptr_t>(p); }
+
+static int compress_params(int mode, CompressParams& cp) {
+  cp.mode = mode;
+  switch (mode) {
+    case CFA_COMPRESS_NONE: cp.thr = 0.0; cp.rep = 0.0; break;
+    case CFA_COMPRESS_SPARSE: cp.thr = 0.001; cp.rep = 0.0001; break;
+    case CFA_COMPRESS_SPARSE_DPCM: cp.thr = 1.e-4; cp.rep = 1.e-4; break;
+    case CFA_COMPRESS_SPARSE_DPCM_HI: cp.thr = 1.e-3; cp.rep = 1.e-3; break;
+    case CFA_COMPRESS_SPARSE_HI: cp.thr = 0.01; cp.rep = 0.001; break;
+    default: return fail(CFA_E_INVALID, "unknown compression mode %d", mode);
+  }
+  return CFA_OK;
+}
+
+// One pass of at most CFA_MAX_FANIN neighbours. Splits the bucket into a scalar head (until
+// every pointer is 16-byte aligned, when they share the same misalignment), a float4 body and
+// a scalar tail. Buckets with different misalignments run entirely on the scalar path.
+static int mix_pass(float* out, const float* local, const float* const* nbrs, const float* c,
+                    int n, size_t P, int rule, const CompressParams* cp, hipStream_t st) {
+  const uintptr_t mis = addr(out) & 15;
+  bool same = (addr(local) & 15) == mis;
+  for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
+  const bool scalar_only = !same || (mis & 3) != 0;
+  size_t head = 0, nvec = 0;
+  if (!scalar_only) {
+    head = mis ? (16 - mis) / 4 : 0;
+    if (head > P) head = P;
+    nvec = (P - head) / 4;
+  } else {
+    head = P;
+  }
+  const size_t tail_begin = head + nvec * 4;
+
+  CompressParams cpv{};
+  if (cp) cpv = *cp;
+
+  if (nvec > 0) {
+    Fanin f{};
+    f.src[0] = local + head;
+    for (int j = 0; j < n; ++j) f.src[j + 1] = nbrs[j] + head;
+    for (int k = 0; k <= n; ++k) f.c[k] = c[k];
+    if (cp) {
+      CompressParams shifted = cpv;
+      shifted.cbegin = cpv.cbegin - (long long)head;
+      shifted.cend = cpv.cend - (long long)head;
+      launch_vec_compress(n, st, out + head, f, (long long)nvec, shifted);
+    } else if (rule == CFA_RULE_SEQUENTIAL) {
+      launch_vec<CFA_RULE_SEQUENTIAL>(n, st, out + head, f, (long long)nvec);
+    } else {
+      launch_vec<CFA_RULE_LINEAR>(n, st, out + head, f, (long long)nvec);
+    }
+    if (int rc = check_launch("mix_vec")) return rc;
+  }
+  // Scalar pieces: [0, head) and [tail_begin, P).
+  const size_t pieces[2][2] = {{0, head}, {tail_begin, P}};
+  for (auto& pc : pieces) {
+    const size_t b = pc[0], e = pc[1];
+    if (e <= b) continue;
+    ScalarFanin sf{};
+    sf.src[0] = local + b;
+    sf.stride[0] = 1;
+    for (int j = 0; j < n; ++j) {
+      sf.src[j + 1] = nbrs[j] + b;
+      sf.stride[j + 1] = 1;
+    }
+    for (int k = 0; k <= n; ++k) sf.c[k] = c[k];
+    sf.n = n;
+    CompressParams sc = cpv;
+    sc.cbegin = cpv.cbegin - (long long)b;
+    sc.cend = cpv.cend - (long long)b;
+    const long long len = (long long)(e - b);
+    mix_scalar_kernel<<<grid_for((len + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        out + b, sf, len, rule, cp ? 1 : 0, sc);
+    if (int rc = check_launch("mix_scalar")) return rc;
+  }
+  return CFA_OK;
+}
+
+static int validate_mix(const float* out, const float* local, const float* const* nbrs, int n,
+                        size_t P) {
+  if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
+  if (P == 0) return CFA_OK;
+  if (!out || !local) return fail(CFA_E_INVALID, "null out/local bucket");
+  if (n > 0 && !nbrs) return fail(CFA_E_INVALID, "null neighbour table");
+  for (int j = 0; j < n; ++j) {
+    if (!nbrs[j]) return fail(CFA_E_INVALID, "null neighbour bucket %d", j);
+    if (nbrs[j] == out) return fail(CFA_E_INVALID, "output aliases neighbour %d", j);
+  }
+  return CFA_OK;
+}
+
+// Sequential rule over any fan-in: chunks of CFA_MAX_FANIN; chunk k>0 continues from `out`.
+// The compression epilogue is fused into the (single) pass when n <= CFA_MAX_FANIN; wider
+// fan-ins run it as a separate pass with the untouched pre-mix `local` as DPCM reference.
+static bool needs_ref(int mode) {
+  return mode == CFA_COMPRESS_SPARSE_DPCM || mode == CFA_COMPRESS_SPARSE_DPCM_HI;
+}
+static int mix_seq_any(float* out, const float* local, const float* const* nbrs,
+                       const float* alphas, int n, size_t P, const CompressParams* cp,
+                       hipStream_t st) {
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  const bool split_epilogue = cp && n > CFA_MAX_FANIN;
+  if (split_epilogue && out == local && needs_ref(cp->mode))
+    return fail(CFA_E_INVALID, "in-place DPCM compression needs fan-in <= %d", CFA_MAX_FANIN);
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = 1.0f;
+    for (int j = 0; j < m; ++j) c[j + 1] = alphas[done + j];
+    const CompressParams* fused = (cp && !split_epilogue) ? cp : nullptr;
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL, fused, st)) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  if (split_epilogue)
+    return cfa_compress_epilogue_f32(out + cp->cbegin, local + cp->cbegin, cp->mode,
+                                     (size_t)(cp->cend - cp->cbegin), cp->kept, st);
+  return CFA_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------
+extern "C" int cfa_mix_seq_f32(float* out, const float* local, const float* const* nbrs,
+                               const float* alphas, int n, size_t P, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,
+                           const float* coeff, int n, size_t P, void* stream) {
+  if (!coeff) return fail(CFA_E_INVALID, "null coefficients");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = done == 0 ? coeff[0] : 1.0f;
+    for (int j = 0; j < m; ++j) c[j + 1] = coeff[done + j + 1];
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_LINEAR, nullptr, st)) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_strided_f32(float* out, const float* local, const float* const* nbrs,
+                                   const int64_t* nbr_stride, const float* alphas, int n, size_t P,
+                                   void* stream) {
+  if (n > 0 && (!alphas || !nbr_stride)) return fail(CFA_E_INVALID, "null alphas/strides");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  bool unit = true;
+  for (int j = 0; j < n; ++j) {
+    if (nbr_stride[j] < 1) return fail(CFA_E_INVALID, "stride %lld < 1", (long long)nbr_stride[j]);
+    unit = unit && nbr_stride[j] == 1;
+  }
+  if (unit) return cfa_mix_seq_f32(out, local, nbrs, alphas, n, P, stream);
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    ScalarFanin sf{};
+    sf.src[0] = w;
+    sf.stride[0] = 1;
+    sf.c[0] = 1.0f;
+    for (int j = 0; j < m; ++j) {
+      sf.src[j + 1] = nbrs[done + j];
+      sf.stride[j + 1] = nbr_stride[done + j];
+      sf.c[j + 1] = alphas[done + j];
+    }
+    sf.n = m;
+    CompressParams none{};
+    mix_scalar_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        out, sf, (long long)P, CFA_RULE_SEQUENTIAL, 0, none);
+    if (int rc = check_launch("mix_strided")) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_seq_compress_f32(float* out, const float* local, const float* const* nbrs,
+                                        const float* alphas, int n, size_t P, int mode,
+                                        size_t cbegin, size_t cend,
+                                        unsigned long long* kept_count, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  if (!kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  cp.cbegin = (long long)cbegin;
+  cp.cend = (long long)cend;
+  cp.kept = kept_count;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    // No neighbours: out = local, then the epilogue (TF1/consensus/cfa_ongraphs.py:218-223).
+    if (out != local && P > 0)
+      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin,
+                                     kept_count, stream);
+  }
+  return mix_seq_any(out, local, nbrs, alphas, n, P, &cp, st);
+}
+
+extern "C" int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, size_t P,
+                                         unsigned long long* kept_count, void* stream) {
+  if (!kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  if ((mode == CFA_COMPRESS_SPARSE_DPCM || mode == CFA_COMPRESS_SPARSE_DPCM_HI) && !ref && P)
+    return fail(CFA_E_INVALID, "DPCM compression needs a reference bucket");
+  if (P == 0) return CFA_OK;
+  if (!y) return fail(CFA_E_INVALID, "null bucket");
+  cp.cbegin = 0;
+  cp.cend = (long long)P;
+  cp.kept = kept_count;
+  hipStream_t st = (hipStream_t)stream;
+  compress_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+      y, ref, (long long)P, cp);
+  return check_launch("compress");
+}
+
+extern "C" int cfa_mewma_update_f32(float* W, float* const* s, const float* const* g,
+                                    const int64_t* g_stride, int n, double rho, float lr1,
+                                    float lr2, size_t lr_split, int init, int use_filtered,
+                                    size_t P, void* stream) {
+  if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
+  if (P == 0 || n == 0) return CFA_OK;
+  if (!W || !s || !g) return fail(CFA_E_INVALID, "null W/s/g");
+  hipStream_t st = (hipStream_t)stream;
+  for (int done = 0; done < n;) {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    MewmaArgs a{};
+    a.W = W;
+    a.n = m;
+    a.rho = (float)rho;
+    a.one_minus_rho = (float)(1.0 - rho);
+    a.lr1 = lr1;
+    a.lr2 = lr2;
+    a.split = (long long)lr_split;
+    a.init = init;
+    a.filtered = use_filtered;
+    bool vec = (addr(W) & 15) == 0;
+    for (int j = 0; j < m; ++j) {
+      if (!s[done + j] || !g[done + j]) return fail(CFA_E_INVALID, "null s/g bucket %d", done + j);
+      a.s[j] = s[done + j];
+      a.g[j] = g[done + j];
+      a.gstride[j] = g_stride ? g_stride[done + j] : 1;
+      if (a.gstride[j] < 1) return fail(CFA_E_INVALID, "gradient stride < 1");
+      vec = vec && a.gstride[j] == 1 && (addr(a.s[j]) & 15) == 0 && (addr(a.g[j]) & 15) == 0;
+    }
+    long long begin = 0;
+    if (vec) {
+      const long long nvec = (long long)P / 4;
+      if (nvec > 0) {
+        mewma_vec_kernel<<<grid_for((nvec + kBlock - 1) / kBlock), kBlock, 0, st>>>(a, nvec);
+        if (int rc = check_launch("mewma_vec")) return rc;
+      }
+      begin = nvec * 4;
+    }
+    if (begin < (long long)P) {
+      mewma_scalar_kernel<<<grid_for(((long long)P - begin + kBlock - 1) / kBlock), kBlock, 0,
+                            st>>>(a, begin, (long long)P);
+      if (int rc = check_launch("mewma_scalar")) return rc;
+    }
+    done += m;
+  }
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                      const int32_t* csr_ptr, const int32_t* csr_idx,
+                                      const float* csr_coef, int D, int rule, size_t P,
+                                      void* stream) {
+  if (D < 0) return fail(CFA_E_INVALID, "negative device count");
+  if (rule != CFA_RULE_SEQUENTIAL && rule != CFA_RULE_LINEAR)
+    return fail(CFA_E_INVALID, "unknown rule %d", rule);
+  if (D == 0 || P == 0) return CFA_OK;
+  if (!out_ptrs || !src_ptrs || !csr_ptr || !csr_idx || !csr_coef)
+    return fail(CFA_E_INVALID, "null population table");
+  if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
+  hipStream_t st = (hipStream_t)stream;
+  // Buckets in a population are expected 16-byte aligned (allocator contract, checked by the
+  // host layer); the body runs on float4, the <4-element tail on the scalar kernel.
+  const long long nvec = (long long)P / 4;
+  if (nvec > 0) {
+    const long long tiles = (nvec + 2LL * kBlock - 1) / (2LL * kBlock);
+    long long gx = tiles;
+    const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+    if (gx > cap) gx = cap < 1 ? 1 : cap;
+    dim3 grid((unsigned)gx, (unsigned)D);
+    if (rule == CFA_RULE_SEQUENTIAL)
+      population_kernel<CFA_RULE_SEQUENTIAL><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                      csr_idx, csr_coef, nvec);
+    else
+      population_kernel<CFA_RULE_LINEAR><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                  csr_idx, csr_coef, nvec);
+    if (int rc = check_launch("population")) return rc;
+  }
+  const long long begin = nvec * 4;
+  if (begin < (long long)P) {
+    dim3 grid(1, (unsigned)D);
+    if (rule == CFA_RULE_SEQUENTIAL)
+      population_tail_kernel<CFA_RULE_SEQUENTIAL><<<grid, 64, 0, st>>>(
+          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
+    else
+      population_tail_kernel<CFA_RULE_LINEAR><<<grid, 64, 0, st>>>(
+          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
+    if (int rc = check_launch("population_tail")) return rc;
+  }
+  return CFA_OK;
+}

@@ -1,0 +1,113 @@
+"""Cross-shard transports for a simulated device population sharded one shard per GPU.
+
+The reference exchanges neighbour models through files on a shared directory (TF1
+``cfa.py:119-130``, TF2 ``consensus_v3.py:82-141``). With the population sharded over the GPUs
+of one node, the only cross-shard traffic of a consensus round is the grouped point-to-point
+halo exchange of boundary buckets; FedAvg sums map to all-reduce.
+
+Two interchangeable transports:
+
+* ``RcclTransport`` — the MI355X path: an RCCL communicator owned by ``libcfa.so``
+  (``cfa_comm_init`` / ``cfa_halo_exchange_f32`` / ``cfa_allreduce_sum_f32``) over xGMI, enqueued
+  on a caller-chosen HIP stream so the exchange overlaps interior mixing on another stream.
+  The 128-byte unique id is broadcast over the existing ``torch.distributed`` group.
+* ``TorchTransport`` — ``torch.distributed`` P2P (``batch_isend_irecv``). With the gloo backend
+  this runs the same sharding logic on CPU tensors (multi-process CPU tests).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Transfer = Tuple[torch.Tensor, int]  # (contiguous buffer, peer rank)
+
+
+class TorchTransport:
+    """torch.distributed point-to-point exchange (any backend; gloo for CPU tests)."""
+
+    name = "torch"
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
+        ops = []
+        for buf, peer in sends:
+            ops.append(dist.P2POp(dist.isend, buf, peer, group=self.group))
+        for buf, peer in recvs:
+            ops.append(dist.P2POp(dist.irecv, buf, peer, group=self.group))
+        if not ops:
+            return
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+    def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+
+    def close(self) -> None:
+        pass
+
+
+class RcclTransport:
+    """RCCL communicator from libcfa.so (one per process/GPU)."""
+
+    name = "rccl"
+
+    def __init__(self, rank: int, world: int, device: int, group=None):
+        from . import _lib
+        self._lib = _lib
+        uid = (ctypes.c_char * _lib.CFA_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            _lib.call("cfa_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
+        payload = [bytes(uid) if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(payload, src=0, group=group)
+        ctypes.memmove(uid, payload[0], _lib.CFA_UNIQUE_ID_BYTES)
+        comm = ctypes.c_void_p()
+        _lib.call("cfa_comm_init", ctypes.byref(comm), rank, world, ctypes.cast(uid, ctypes.c_void_p),
+                  int(device))
+        self.comm = comm
+        self.rank, self.world, self.device = rank, world, device
+
+    @staticmethod
+    def _stream(stream) -> int:
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return int(s.cuda_stream)
+
+    def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
+        """Enqueue the grouped exchange on ``stream`` (asynchronous). All buffers must have the
+        same element count; the caller orders stream dependencies."""
+        if not sends and not recvs:
+            return
+        counts = {b.numel() for b, _ in list(sends) + list(recvs)}
+        if len(counts) != 1:
+            raise ValueError("halo buffers must all have the same length")
+        for b, _ in list(sends) + list(recvs):
+            if not (b.is_cuda and b.dtype == torch.float32 and b.is_contiguous()):
+                raise TypeError("halo buffers must be contiguous fp32 CUDA tensors")
+        L = self._lib
+        L.call("cfa_halo_exchange_f32", self.comm, L.ptr_table([b.data_ptr() for b, _ in sends]),
+               L.int_array([p for _, p in sends]), len(sends),
+               L.ptr_table([b.data_ptr() for b, _ in recvs]), L.int_array([p for _, p in recvs]),
+               len(recvs), counts.pop(), self._stream(stream))
+
+    def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
+        self._lib.call("cfa_allreduce_sum_f32", self.comm, buf.data_ptr(), buf.data_ptr(), buf.numel(),
+                       self._stream(stream))
+
+    def close(self) -> None:
+        if self.comm:
+            self._lib.call("cfa_comm_destroy", self.comm)
+            self.comm = None
+
+
+def make_transport(kind: str, rank: int, world: int, device: Optional[int] = None, group=None):
+    if kind == "rccl":
+        return RcclTransport(rank, world, device if device is not None else torch.cuda.current_device(),
+                             group)
+    if kind == "torch":
+        return TorchTransport(group)
+    raise ValueError(f"unknown transport {kind!r}")

@@ -1,0 +1,232 @@
+"""Device-level consensus engine: the libcfa kernels on PyTorch-ROCm tensors.
+
+PyTorch provides device memory and streams only; all arithmetic runs in the HIP kernels of
+``libcfa.so`` (``federated_amd/csrc/cfa_engine.hip``). Every call is asynchronous on the
+given stream (default: torch's current stream on the tensor's device).
+
+A *bucket* is a 1-D contiguous fp32 CUDA tensor holding one model (or gradient) flattened
+layer by layer in the order the reference passes its tensors; ``BucketLayout`` maps the
+reference's per-layer arrays to and from that flat form.
+"""
+from __future__ import annotations
+
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+
+__all__ = ["Engine", "BucketLayout", "get_engine"]
+
+
+def _require_gpu(device: Optional[torch.device]) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("federated_amd: no ROCm GPU visible; the consensus engine runs only on "
+                           "MI355X (gfx950) through libcfa.so and has no CPU fallback")
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError(f"engine device must be a cuda device, got {device}")
+    return torch.device("cuda", device.index if device.index is not None else torch.cuda.current_device())
+
+
+def _check_bucket(t: torch.Tensor, name: str, P: Optional[int] = None) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must live on the GPU (got {t.device})")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    n = t.numel()
+    if P is not None and n != P:
+        raise ValueError(f"{name} has {n} elements, expected {P}")
+    return n
+
+
+class BucketLayout:
+    """Offsets of a list of tensors flattened into one bucket (layer order preserved)."""
+
+    def __init__(self, shapes: Iterable[Sequence[int]]):
+        self.shapes = [tuple(int(d) for d in s) for s in shapes]
+        self.sizes = [int(np.prod(s)) if len(s) else 1 for s in self.shapes]
+        self.offsets = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
+        self.P = int(self.offsets[-1])
+
+    @classmethod
+    def of(cls, arrays) -> "BucketLayout":
+        return cls([np.shape(a) for a in arrays])
+
+    def segment(self, k: int) -> tuple:
+        return int(self.offsets[k]), int(self.offsets[k + 1])
+
+    def pack(self, arrays, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Flatten per-layer arrays into ``out`` (fp32, length P), converting dtype if needed."""
+        if out is None:
+            out = np.empty(self.P, dtype=np.float32)
+        if len(arrays) != len(self.sizes):
+            raise ValueError(f"expected {len(self.sizes)} tensors, got {len(arrays)}")
+        for k, a in enumerate(arrays):
+            a = np.asarray(a)
+            if a.size != self.sizes[k]:
+                raise ValueError(f"tensor {k} has {a.size} elements, layout expects {self.sizes[k]}")
+            b, e = self.segment(k)
+            out[b:e] = a.reshape(-1)
+        return out
+
+    def unpack(self, flat: np.ndarray, copy: bool = True) -> list:
+        res = []
+        for k, shp in enumerate(self.shapes):
+            b, e = self.segment(k)
+            v = flat[b:e].reshape(shp)
+            res.append(v.copy() if copy else v)
+        return res
+
+
+class Engine:
+    """libcfa kernels bound to one GPU."""
+
+    def __init__(self, device=None):
+        self.device = _require_gpu(device)
+        self.lib = _lib.load()
+
+    # -- helpers ---------------------------------------------------------------------------
+    def stream_handle(self, stream: Optional[torch.cuda.Stream] = None) -> int:
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return int(s.cuda_stream)
+
+    def empty(self, P: int) -> torch.Tensor:
+        return torch.empty(P, dtype=torch.float32, device=self.device)
+
+    def counter(self) -> torch.Tensor:
+        return torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    # -- mixing ----------------------------------------------------------------------------
+    def mix_seq(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                alphas: Sequence[float], stream=None) -> torch.Tensor:
+        """out = fold_j(w <- w + alphas[j]*(nbrs[j] - w)), w0 = local (sequential CFA rule)."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P)
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
+        _lib.call("cfa_mix_seq_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(alphas),
+                  len(nbrs), P, self.stream_handle(stream))
+        return out
+
+    def mix_linear(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                   coeff: Sequence[float], stream=None) -> torch.Tensor:
+        """out = coeff[0]*local + sum_j coeff[j+1]*nbrs[j]."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P)
+        if len(coeff) != len(nbrs) + 1:
+            raise ValueError("len(coeff) must be len(nbrs) + 1")
+        _lib.call("cfa_mix_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(coeff),
+                  len(nbrs), P, self.stream_handle(stream))
+        return out
+
+    def mix_strided(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                    alphas: Sequence[float], stream=None) -> torch.Tensor:
+        """Sequential mix where neighbour j may be a 1-D strided view (e.g. g[..., ii])."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        strides = []
+        for j, x in enumerate(nbrs):
+            if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 1 or x.numel() != P:
+                raise ValueError(f"nbrs[{j}] must be a 1-D fp32 CUDA view of {P} elements")
+            strides.append(int(x.stride(0)))
+        _lib.call("cfa_mix_strided_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.int64_array(strides),
+                  _lib.float_array(alphas), len(nbrs), P, self.stream_handle(stream))
+        return out
+
+    def mix_seq_compress(self, out: torch.Tensor, local: torch.Tensor,
+                         nbrs: Sequence[torch.Tensor], alphas: Sequence[float], mode: int,
+                         cbegin: int, cend: int, kept: torch.Tensor, stream=None) -> torch.Tensor:
+        """Sequential mix fused with the cfa_ongraphs compression epilogue on [cbegin, cend).
+        Adds the kept-parameter count to ``kept`` (int64 CUDA tensor of one element)."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P)
+        self._check_counter(kept)
+        _lib.call("cfa_mix_seq_compress_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(alphas),
+                  len(nbrs), P, int(mode), int(cbegin), int(cend), kept.data_ptr(),
+                  self.stream_handle(stream))
+        return out
+
+    def compress(self, y: torch.Tensor, ref: Optional[torch.Tensor], mode: int,
+                 kept: torch.Tensor, stream=None) -> torch.Tensor:
+        P = _check_bucket(y, "y")
+        if ref is not None:
+            _check_bucket(ref, "ref", P)
+        self._check_counter(kept)
+        _lib.call("cfa_compress_epilogue_f32", y.data_ptr(), ref.data_ptr() if ref is not None else None,
+                  int(mode), P, kept.data_ptr(), self.stream_handle(stream))
+        return y
+
+    @staticmethod
+    def _check_counter(kept: torch.Tensor) -> None:
+        if not (isinstance(kept, torch.Tensor) and kept.is_cuda and kept.dtype == torch.int64
+                and kept.numel() >= 1):
+            raise TypeError("kept must be an int64 CUDA tensor")
+
+    # -- CFA-GE ----------------------------------------------------------------------------
+    def mewma(self, W: torch.Tensor, s: Sequence[torch.Tensor], g: Sequence[torch.Tensor],
+              rho: float, lr1: float, lr2: float, lr_split: int, init: bool, use_filtered: bool,
+              stream=None) -> torch.Tensor:
+        """CFA-GE update: for each j, s_j <- init ? g_j : rho*g_j + (1-rho)*s_j;
+        W <- W - lr*(use_filtered ? s_j : g_j) with lr = lr1 below lr_split, lr2 above."""
+        P = _check_bucket(W, "W")
+        if len(s) != len(g):
+            raise ValueError("one state bucket per gradient bucket")
+        strides = []
+        for j in range(len(g)):
+            _check_bucket(s[j], f"s[{j}]", P)
+            gj = g[j]
+            if not gj.is_cuda or gj.dtype != torch.float32 or gj.dim() != 1 or gj.numel() != P:
+                raise ValueError(f"g[{j}] must be a 1-D fp32 CUDA view of {P} elements")
+            strides.append(int(gj.stride(0)))
+        _lib.call("cfa_mewma_update_f32", W.data_ptr(), _lib.ptr_table([x.data_ptr() for x in s]),
+                  _lib.ptr_table([x.data_ptr() for x in g]), _lib.int64_array(strides), len(g),
+                  float(rho), float(lr1), float(lr2), int(lr_split), int(bool(init)),
+                  int(bool(use_filtered)), P, self.stream_handle(stream))
+        return W
+
+    # -- population ------------------------------------------------------------------------
+    def population(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
+                   csr_idx: torch.Tensor, csr_coef: torch.Tensor, D: int, rule: int, P: int,
+                   stream=None) -> None:
+        """One launch mixing D devices; tables are device tensors (int64 pointers, int32 CSR,
+        fp32 coefficients). See cfa_mix_population_f32."""
+        for name, t, dt in (("out_ptrs", out_ptrs, torch.int64), ("src_ptrs", src_ptrs, torch.int64),
+                            ("csr_ptr", csr_ptr, torch.int32), ("csr_idx", csr_idx, torch.int32),
+                            ("csr_coef", csr_coef, torch.float32)):
+            if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+                raise TypeError(f"{name} must be a contiguous {dt} CUDA tensor")
+        if csr_ptr.numel() != D + 1 or out_ptrs.numel() != D:
+            raise ValueError("csr_ptr must have D+1 entries and out_ptrs D entries")
+        _lib.call("cfa_mix_population_f32", out_ptrs.data_ptr(), src_ptrs.data_ptr(),
+                  csr_ptr.data_ptr(), csr_idx.data_ptr(), csr_coef.data_ptr(), int(D), int(rule),
+                  int(P), self.stream_handle(stream))
+
+
+_engines: dict = {}
+
+
+def get_engine(device=None) -> Engine:
+    """Process-wide engine per device (the engine object itself holds no mutable state)."""
+    dev = _require_gpu(device)
+    eng = _engines.get(dev.index)
+    if eng is None:
+        eng = _engines[dev.index] = Engine(dev)
+    return eng

@@ -1,0 +1,167 @@
+/*
+ * cfa_engine.h — C-ABI of libcfa.so, the MI355X (gfx950) consensus-reduction engine.
+ *
+ * This is the drop-in boundary for the CFA / CFA-GE neighbour-model mixing step of
+ * labRadioVision/federated. The reference computes that step with numpy AXPY chains
+ * inside its `consensus` package. Each entry point below replaces one of those chains
+ * (citations are `path:line` under the reference tree; TF1 = tensorflow1_implementations,
+ * TF2 = tensorflow2_implementations/MNIST_dataset unless stated).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. Buffers are caller-owned device pointers
+ *     (hipMalloc / PyTorch-ROCm tensors). The library allocates nothing on the hot path.
+ *   - `stream` is a hipStream_t passed as void*; NULL means the legacy default stream.
+ *     Every compute call is asynchronous on that stream.
+ *   - Return 0 on success, a negative CFA_E* code on failure. `cfa_last_error()` returns a
+ *     thread-local message for the last failure on the calling thread. No exceptions cross
+ *     the ABI. The library keeps no global mutable state: calls are re-entrant.
+ *   - `P` is the bucket length in fp32 elements. A "bucket" is one model (or gradient)
+ *     flattened layer by layer, in the order the reference passes its tensors.
+ *   - Pointer arrays (`nbrs`, `alphas`, `coeff`, `s`, `g`) are HOST arrays whose entries are
+ *     device pointers (or host scalars for coefficients).
+ *   - `out` may alias `local` / `W` (in-place update). Outputs must not alias any neighbour.
+ *   - Any fan-in n >= 0 is accepted; n > CFA_MAX_FANIN is executed as several passes.
+ */
+#ifndef CFA_ENGINE_H
+#define CFA_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define CFA_API __attribute__((visibility("default")))
+#else
+#define CFA_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFA_VERSION 10000 /* 1.0.0 */
+#define CFA_MAX_FANIN 16  /* neighbours folded per kernel pass */
+
+enum {
+  CFA_OK = 0,
+  CFA_E_INVALID = -1,     /* bad argument (null pointer, negative size, bad mode) */
+  CFA_E_HIP = -2,         /* HIP runtime error (launch, memcpy, device) */
+  CFA_E_RCCL = -3,        /* RCCL error */
+  CFA_E_UNSUPPORTED = -4  /* feature not available in this build */
+};
+
+/* Mixing rules. */
+enum {
+  /* Sequential CFA rule: w <- w + a_j * (x_j - w), j = 0..n-1, evaluated as
+   * t = x_j - w; t = a_j * t; w = w + t (three fp32 roundings, no FMA contraction).
+   * This reproduces the fp32 numpy chain bit for bit. */
+  CFA_RULE_SEQUENTIAL = 0,
+  /* Linear combination: out = c_0 * local + sum_j c_{j+1} * x_j (fp32 FMA chain). */
+  CFA_RULE_LINEAR = 1
+};
+
+/* Compression epilogue modes (TF1/consensus/cfa_ongraphs.py:225-273). */
+enum {
+  CFA_COMPRESS_NONE = 0,
+  CFA_COMPRESS_SPARSE = 1,          /* |y| < 1e-3 -> sign(y) * 1e-4                       :227-237 */
+  CFA_COMPRESS_SPARSE_DPCM = 2,     /* |y - ref| < 1e-4 -> ref + sign(y - ref) * 1e-4      :239-249 */
+  CFA_COMPRESS_SPARSE_DPCM_HI = 3,  /* |y - ref| < 1e-3 -> ref + sign(y - ref) * 1e-3      :250-260 */
+  CFA_COMPRESS_SPARSE_HI = 4        /* |y| < 1e-2 -> sign(y) * 1e-3                        :261-271 */
+};
+
+CFA_API int cfa_version(void);
+CFA_API const char* cfa_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.
+ *   out[i] = fold_j( w <- w + alphas[j] * (nbrs[j][i] - w) ), w0 = local[i]
+ * Replaces:
+ *   TF1/consensus/cfa.py:66-76 (per-neighbour loop :119-130, alpha = eps/N)
+ *   TF1/consensus/cfa_ongraphs.py:109-119 (loop :196-213, alpha = eps/(1+n))
+ *   TF1/consensus/cfa_mobilenet.py:82-91, cfa_ge_2stage.py:73-83 (stage 1, :449-466)
+ *   TF2 consensus_v3.py:153-155 / consensus_v2.py:153-155 / consensus_v4.py:211-213 (weights)
+ *   TF2 consensus_v3.py:236-238 / consensus_v4.py:251-253 (gradients)
+ *   TF2/FL_over_MQTT/learner_consensus.py:150-153 (alpha = 1/2)
+ * Bytes moved: (n + 2) * P * 4.
+ */
+CFA_API int cfa_mix_seq_f32(float* out, const float* local, const float* const* nbrs,
+                    const float* alphas, int n, size_t P, void* stream);
+
+/* Linear-combination mix: out[i] = coeff[0]*local[i] + sum_j coeff[j+1]*nbrs[j][i].
+ * The closed form of the sequential rule (c_0 = prod(1-a_j), c_{j+1} = a_j prod_{k>j}(1-a_k)),
+ * and the FedAvg / parameter-server aggregation shape
+ * (TF2 parameter_server_v2.py:159-161, PS_server.py:127-134). */
+CFA_API int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,
+                const float* coeff, int n, size_t P, void* stream);
+
+/* Sequential mix with element-strided neighbour buckets: element i of neighbour j is read at
+ * nbrs[j][i * nbr_stride[j]]. Serves the `[..., devices]` gradient slices of CFA-GE
+ * (TF1/consensus/cfa_ge_2stage.py:594-606, slice `[..., ii]`, stride = devices). */
+CFA_API int cfa_mix_strided_f32(float* out, const float* local, const float* const* nbrs,
+                        const int64_t* nbr_stride, const float* alphas, int n, size_t P,
+                        void* stream);
+
+/* Sequential mix fused with the compression epilogue of cfa_ongraphs.py:225-273.
+ * The epilogue applies to elements [cbegin, cend) of the bucket (the W2 tensor), with
+ * `local` as the DPCM reference (n_W_l2 is the pre-mix local, :246-247). The number of
+ * elements in that range NOT replaced is ADDED to *kept_count (a device uint64; zero it
+ * first). Mode CFA_COMPRESS_NONE adds (cend - cbegin). */
+CFA_API int cfa_mix_seq_compress_f32(float* out, const float* local, const float* const* nbrs,
+                             const float* alphas, int n, size_t P, int mode, size_t cbegin,
+                             size_t cend, unsigned long long* kept_count, void* stream);
+
+/* (a3) Standalone compression epilogue, in place on y[0..P), reference `ref` (may be NULL
+ * for modes 1/4). Adds the kept count to *kept_count (device uint64). */
+CFA_API int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, size_t P,
+                              unsigned long long* kept_count, void* stream);
+
+/* (a4) CFA-GE gradient-bucket update (MEWMA), for j = 0..n-1 in order:
+ *   s_j <- init ? g_j : rho*g_j + (1-rho)*s_j
+ *   W   <- W - lr(i) * (use_filtered ? s_j : g_j),   lr(i) = i < lr_split ? lr1 : lr2
+ * Replaces TF1/consensus/cfa_ge_2stage.py:593-621 (fast; CNN use_filtered=1, 2NN 0) and
+ * :329-371 (4-stage: init=1 at epoch 1, use_filtered=0). W and s_j are updated in place.
+ * g_j is read with element stride g_stride (1 = contiguous). rho is a double so that rho and
+ * (1 - rho) are each rounded once to fp32, as numpy does with a Python-float hyperparameter.
+ * Bytes moved: (3n + 2) * P * 4. */
+CFA_API int cfa_mewma_update_f32(float* W, float* const* s, const float* const* g,
+                         const int64_t* g_stride, int n, double rho, float lr1, float lr2,
+                         size_t lr_split, int init, int use_filtered, size_t P, void* stream);
+
+/* (a1-a6 batched) Population round: one launch mixes D devices.
+ * For device d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]) list its sources in order; the
+ * FIRST entry is the device's own (local) bucket. Source e is src_ptrs[csr_idx[e]], output d
+ * is out_ptrs[d]; both tables are DEVICE arrays of device pointers. rule:
+ *   CFA_RULE_SEQUENTIAL: w = src(first); w <- w + csr_coef[e]*(src(e) - w) for later e
+ *   CFA_RULE_LINEAR:     out = sum_e csr_coef[e] * src(e)
+ * csr_ptr/csr_idx/csr_coef are DEVICE arrays. Outputs must not alias any source. */
+CFA_API int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                           const int32_t* csr_ptr, const int32_t* csr_idx,
+                           const float* csr_coef, int D, int rule, size_t P, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Multi-GPU (RCCL over xGMI): one process per GPU.
+ * The reference has no collectives; its cross-device edges are files polled on a shared
+ * directory (TF1/consensus/cfa.py:119-130, TF2 consensus_v3.py:82-141). When the simulated
+ * population is sharded over the GPUs of one node those edges become RCCL transfers.
+ */
+#define CFA_UNIQUE_ID_BYTES 128
+
+/* Fill `id` (CFA_UNIQUE_ID_BYTES bytes) on one rank; share it with the others out of band. */
+CFA_API int cfa_comm_unique_id(void* id);
+/* Create a communicator for `rank` of `nranks` on HIP device `device`. */
+CFA_API int cfa_comm_init(void** comm, int rank, int nranks, const void* id, int device);
+CFA_API int cfa_comm_destroy(void* comm);
+/* Grouped point-to-point halo exchange of whole buckets: send_bufs[i] (P floats) goes to
+ * rank send_peers[i], recv_bufs[i] is filled from recv_peers[i]. One RCCL group. */
+CFA_API int cfa_halo_exchange_f32(void* comm, const float* const* send_bufs, const int* send_peers,
+                          int nsend, float* const* recv_bufs, const int* recv_peers, int nrecv,
+                          size_t P, void* stream);
+/* Sum all-reduce / reduce of pre-scaled buckets (FedAvg / parameter-split sums). */
+CFA_API int cfa_allreduce_sum_f32(void* comm, const float* send, float* recv, size_t count,
+                          void* stream);
+CFA_API int cfa_reduce_sum_f32(void* comm, const float* send, float* recv, size_t count, int root,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFA_ENGINE_H */

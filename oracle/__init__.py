@@ -1,0 +1,3 @@
+"""ORACLE — test infrastructure only (CPU restatement of the reference arithmetic).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg."""

@@ -1,0 +1,223 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY. Not part of the product.
+
+CPU (numpy) restatement of the reference's consensus arithmetic, used as the parity checker
+for the HIP kernels in ``libcfa.so``. Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import this module, and only as the checker or as the
+timed CPU baseline. The product path (``federated_amd``) never imports it.
+
+Each function restates one reference code path with the same operation order and the same
+numpy dtype rules (numpy 2 / NEP 50 promotion), citing the reference file:line it follows
+(paths under labRadioVision/federated; TF1 = tensorflow1_implementations,
+TF2 = tensorflow2_implementations/MNIST_dataset unless stated).
+
+Pinning: every function here is checked against golden vectors produced by running the
+reference code itself (``tests/golden/make_golden.py``) in ``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import List, Sequence
+
+import numpy as np
+
+# ----------------------------------------------------------------------------------------
+# Generic sequential rule (the TF2 idiom, fp32 in / fp32 out)
+# ----------------------------------------------------------------------------------------
+
+
+def sequential_mix(local: np.ndarray, nbrs: Sequence[np.ndarray], alphas: Sequence[float]) -> np.ndarray:
+    """w <- w + a_j * (x_j - w) for j in order (TF2 consensus_v3.py:153-155).
+
+    ``a_j`` are Python floats, so under NEP 50 they are cast to the array dtype (fp32 for fp32
+    buckets) exactly as in the reference."""
+    w = local
+    for x, a in zip(nbrs, alphas):
+        w = w + a * (x - w)
+    return w
+
+
+def closed_form_coeffs(alphas: Sequence[float]) -> List[float]:
+    """Coefficients of out = c0*local + sum_j c_{j+1} x_j equal to the sequential rule:
+    c0 = prod(1 - a_j), c_{j+1} = a_j * prod_{k>j} (1 - a_k)."""
+    n = len(alphas)
+    c = [0] * (n + 1)
+    tail = 1
+    for j in range(n - 1, -1, -1):
+        c[j + 1] = alphas[j] * tail
+        tail *= 1 - alphas[j]
+    c[0] = tail
+    return c
+
+
+# ----------------------------------------------------------------------------------------
+# TF2 consensus_v2/v3/v4 (a5, a6)
+# ----------------------------------------------------------------------------------------
+
+
+def tf2_weights(local_layers, nbr_models, training_end: bool = False) -> list:
+    """consensus_v3.py:144-159 (= v2 :144-159, v4 :202-217): eps <- 1/(len(nbrs)+1)
+    (overrides the argument, :145); if training_end the local model becomes the LAST received
+    neighbour (:147-152); else per neighbour q and layer k: w[k] <- w[k] + eps*(x_q[k] - w[k]).
+    Returns the list the reference returns (``self.local_weights.tolist()``)."""
+    w = list(local_layers)
+    if len(nbr_models) > 0:
+        eps = 1 / (len(nbr_models) + 1)
+        for q in range(len(nbr_models)):
+            if training_end:
+                for k in range(len(w)):
+                    w[k] = nbr_models[-1][k]
+                break
+            for k in range(len(w)):
+                w[k] = w[k] + eps * (nbr_models[q][k] - w[k])
+    return w
+
+
+def tf2_grads_v3(local_grads, nbr_grads) -> list:
+    """consensus_v3.py:232-245: eps <- 1/(len+1) (override, :233), sequential rule per layer."""
+    g = list(local_grads)
+    if len(nbr_grads) > 0:
+        eps = 1 / (len(nbr_grads) + 1)
+        for q in range(len(nbr_grads)):
+            for k in range(len(g)):
+                g[k] = g[k] + eps * (nbr_grads[q][k] - g[k])
+    return g
+
+
+def tf2_grads_v4(local_grads, nbr_grads, eps: float) -> list:
+    """consensus_v4.py:247-260: the caller's eps is used as given (the override is commented
+    out at :248)."""
+    g = list(local_grads)
+    for q in range(len(nbr_grads)):
+        for k in range(len(g)):
+            g[k] = g[k] + eps * (nbr_grads[q][k] - g[k])
+    return g
+
+
+# ----------------------------------------------------------------------------------------
+# TF1 consensus package (a1, a2, a3, a4)
+# ----------------------------------------------------------------------------------------
+
+
+def tf1_weight_factor(devices: int, ii: int, ii2: int, denom_neighbors: int) -> np.float64:
+    """Equation (11) as coded: b = 1/devices; b_j / (b_j + m * b_i) with m = N-1 in cfa.py:66-68
+    and cfa_ge_2stage.py:73-75, m = n (this call's neighbour count) in cfa_ongraphs.py:109-111."""
+    b_v = 1 / devices
+    balancing_vect = np.ones(devices) * b_v
+    return balancing_vect[ii2] / (balancing_vect[ii2] + denom_neighbors * balancing_vect[ii])
+
+
+def tf1_mix(local4, nbr4_list, eps: float, factors) -> list:
+    """Sequential TF1 mix of the 4 tensors (W1, b1, W2, b2) (cfa.py:69-76 and the same lines in
+    cfa_ongraphs.py:112-119 / cfa_ge_2stage.py:76-83): w <- w + eps*wf_j*(x_j - w).
+    Under numpy 2, ``eps*wf`` is an np.float64, so every step after the first subtraction is
+    fp64 (as in the reference). Returns [W1, b1, W2, b2] with biases squeezed
+    (cfa.py:141-144)."""
+    w = [np.asarray(t) for t in local4]
+    for x4, wf in zip(nbr4_list, factors):
+        w = [w[k] + eps * wf * (np.asarray(x4[k]) - w[k]) for k in range(4)]
+    return [np.asarray(w[0]), np.squeeze(np.asarray(w[1])), np.asarray(w[2]), np.squeeze(np.asarray(w[3]))]
+
+
+COMPRESSION = {  # cfa_ongraphs.py:227-271: (threshold, replacement, differential)
+    1: (0.001, 0.0001, False),
+    2: (1.e-4, 1.e-4, True),
+    3: (1.e-3, 1.e-3, True),
+    4: (0.01, 0.001, False),
+}
+
+
+def tf1_compress(W_up_l2: np.ndarray, n_W_l2: np.ndarray, mode: int):
+    """Vectorised restatement of the compression double loop cfa_ongraphs.py:225-273.
+    Modifies ``W_up_l2`` in place (as the reference does) and returns counter_param."""
+    if mode not in COMPRESSION:
+        return W_up_l2.shape[0] * W_up_l2.shape[1]
+    thr, rep, diff = COMPRESSION[mode]
+    if diff:
+        d = W_up_l2 - n_W_l2
+        mask = np.abs(d) < thr
+        W_up_l2[mask] = n_W_l2[mask] + np.sign(d[mask]) * rep
+    else:
+        mask = np.abs(W_up_l2) < thr
+        W_up_l2[mask] = np.sign(W_up_l2[mask]) * rep
+    return int(np.count_nonzero(~mask))
+
+
+def tf1_datagrad_slice(datagrad4, ii: int) -> list:
+    """Slot ``ii`` of a neighbour's datagrad tensors (cfa_ge_2stage.py:575-589): the weight
+    gradients are [..., devices] arrays read as ``g[..., ii]``; the bias gradients are squeezed
+    first (:578-579)."""
+    return [np.asarray(datagrad4[0])[..., ii], np.squeeze(np.asarray(datagrad4[1]))[..., ii],
+            np.asarray(datagrad4[2])[..., ii], np.squeeze(np.asarray(datagrad4[3]))[..., ii]]
+
+
+def tf1_mewma(W4, states4, grads4_list, rho: float, lr1: float, lr2: float,
+              use_filtered: bool, init: bool) -> list:
+    """CFA-GE gradient step (cfa_ge_2stage.py:591-621 fast; :329-371 4-stage), for neighbour
+    j in order with its slot-ii gradients ``grads4_list[j]`` = [gW1, gb1, gW2, gb2]:
+      s_j <- g_j (4-stage, epoch 1: init=True) or rho*g_j + (1-rho)*s_j (MEWMA);
+      W   <- W - lr * (s_j if use_filtered else g_j), lr = lr1 (layer 1) / lr2 (layer 2).
+    ``states4`` are the caller's [..., N] saved-state arrays, updated in place at slot j.
+    use_filtered: CNN fast path only (:603-606); 2NN fast (:618-621) and 4-stage (:347-350)
+    subtract the raw gradient."""
+    W = list(W4)
+    lrs = (lr1, lr1, lr2, lr2)
+    for j, g4 in enumerate(grads4_list):
+        for k in range(4):
+            g = g4[k]
+            s = states4[k]
+            if init:
+                s[..., j] = g
+            else:
+                s[..., j] = rho * g + (1 - rho) * s[..., j]
+            W[k] = W[k] - lrs[k] * (s[..., j] if use_filtered else g)
+    return W
+
+
+# ----------------------------------------------------------------------------------------
+# Neighbour selection (a7)
+# ----------------------------------------------------------------------------------------
+
+
+def tf1_kregular(ii: int, neighbors: int, devices: int) -> np.ndarray:
+    """cfa.py:14-32 (identical in cfa_ongraphs.py:54-72, cfa_ge_2stage.py:14-32)."""
+    if ii == 0:
+        return np.arange(ii + 1, ii + neighbors + 1)
+    if ii == devices - 1:
+        return np.arange(ii - neighbors, ii)
+    if ii >= math.ceil(neighbors / 2) and ii <= devices - math.ceil(neighbors / 2) - 1:
+        s = np.arange(ii - math.floor(neighbors / 2), ii + math.floor(neighbors / 2) + 1)
+    elif ii - math.ceil(neighbors / 2) < 0:
+        s = np.arange(0, neighbors + 1)
+    else:
+        s = np.arange(devices - neighbors - 1, devices)
+    return np.delete(s, np.where(s == ii))
+
+
+def tf2_kregular_v3(ii: int, neighbors: int, devices: int) -> np.ndarray:
+    """consensus_v3.py:44-70: at least 2 neighbours."""
+    return tf1_kregular(ii, max(neighbors, 2), devices)
+
+
+def tf2_kregular_v4(ii: int, neighbors: int, devices: int):
+    """consensus_v4.py:111-141: N < 2 -> ring in-neighbour ii-1 (0 -> devices-1), a scalar."""
+    if neighbors < 2:
+        return ii - 1 if ii > 0 else devices - 1
+    return tf1_kregular(ii, neighbors, devices)
+
+
+def tf2_tx_v4(ii: int, neighbors: int, devices: int):
+    """consensus_v4.py:143-173: N < 2 -> ring out-neighbour ii+1 (devices-1 -> 0)."""
+    if neighbors < 2:
+        return 0 if ii == devices - 1 else ii + 1
+    return tf1_kregular(ii, neighbors, devices)
+
+
+def mobile_neighbors(graph: np.ndarray, ii: int, max_neighbors: int, devices: int, g: int) -> np.ndarray:
+    """cfa_ongraphs.py:33-52: row ii of adjacency g, then random.choices(k=max) (WITH
+    replacement, Python ``random``) if there are more than max_neighbors."""
+    row = graph[ii, :, g]
+    nb = np.asarray([kk for kk in range(devices) if row[kk] == 1], dtype=np.uint8)
+    if nb.size > max_neighbors:
+        return np.asarray(random.choices(nb, k=max_neighbors))
+    return nb

@@ -1,0 +1,91 @@
+"""CPU checks of the C-ABI boundary: libcfa.so loads, exports every symbol include/cfa_engine.h
+declares, and the ctypes table matches the header one for one. No compute calls (no GPU)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "cfa_engine.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"CFA_API\s+[\w\s\*]+?\b(cfa_\w+)\s*\(", text)))
+
+
+def test_header_declares_full_abi():
+    syms = header_symbols()
+    for required in ("cfa_mix_seq_f32", "cfa_mix_f32", "cfa_mix_strided_f32", "cfa_mewma_update_f32",
+                     "cfa_compress_epilogue_f32", "cfa_mix_population_f32", "cfa_comm_init",
+                     "cfa_halo_exchange_f32", "cfa_allreduce_sum_f32", "cfa_last_error", "cfa_version"):
+        assert required in syms
+
+
+def test_library_exports_every_header_symbol():
+    from federated_amd import _lib
+    lib = _lib.load()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\sT\s+(cfa_\w+)", out))
+    assert set(header_symbols()) <= exported
+    for name in header_symbols():
+        assert hasattr(lib, name)
+
+
+def test_ctypes_table_matches_header():
+    from federated_amd import _lib
+    assert sorted(_lib.SIGNATURES) == header_symbols()
+    text = open(HEADER).read()
+    for name, (_, args) in _lib.SIGNATURES.items():
+        m = re.search(r"\b%s\s*\(([^)]*)\)" % name, text, re.S)
+        decl = m.group(1).strip()
+        nargs = 0 if decl in ("", "void") else decl.count(",") + 1
+        assert nargs == len(args), name
+
+
+def test_version_and_error_calls_without_gpu():
+    from federated_amd import _lib
+    lib = _lib.load()
+    assert lib.cfa_version() == 10000
+    assert isinstance(lib.cfa_last_error(), bytes)
+
+
+def test_invalid_arguments_fail_loudly_before_any_device_work():
+    """Argument validation runs on the host: a bad call returns CFA_E_INVALID and the shim
+    raises with the library's message (no device touched for these)."""
+    from federated_amd import _lib
+    with pytest.raises(_lib.CFAError, match="negative fan-in"):
+        _lib.call("cfa_mix_seq_f32", 1 << 20, 1 << 20, None, _lib.float_array([0.5]), -1, 16, None)
+    with pytest.raises(_lib.CFAError, match="unknown compression mode"):
+        _lib.call("cfa_compress_epilogue_f32", 1 << 20, None, 9, 16, 1 << 21, None)
+    with pytest.raises(_lib.CFAError, match="null communicator"):
+        _lib.call("cfa_allreduce_sum_f32", None, None, None, 4, None)
+
+
+def test_single_hip_runtime_in_process():
+    """libcfa must bind to the HIP runtime torch loaded (one libamdhip64 mapped)."""
+    import torch  # noqa: F401
+    from federated_amd import _lib
+    _lib.load()
+    assert len(_lib.loaded_hip_runtimes()) == 1, _lib.loaded_hip_runtimes()
+
+
+def test_product_has_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from federated_amd.engine import get_engine
+    with pytest.raises(RuntimeError, match="no ROCm GPU"):
+        get_engine()
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "federated_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f

@@ -1,0 +1,204 @@
+"""GPU parity of the libcfa kernels against the CPU oracle, called through the C-ABI.
+
+Bars: the sequential rule is bit-exact against fp32 numpy (same three roundings);
+the linear closed form and the fp64-reference TF1 paths are within 1e-5 normwise
+(max|y - r| <= 1e-5 * max|r|); compression counts are exact integers."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import normwise_close
+from oracle import cfa_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _rand(rng, n, P, scale=1.0):
+    return [(rng.standard_normal(P) * scale).astype(np.float32) for _ in range(n)]
+
+
+SIZES = [0, 1, 3, 4, 5, 255, 1023, 4096 + 3, 1 << 20, 3 * (1 << 20) + 7]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 8, 16, 17, 33])
+def test_mix_seq_bitexact(gpu, n):
+    rng = np.random.default_rng(100 + n)
+    for P in SIZES:
+        local = _rand(rng, 1, P)[0]
+        nbrs = _rand(rng, n, P)
+        alphas = [1.0 / (n + 1)] * n if n else []
+        ref = O.sequential_mix(local, nbrs, alphas)
+        out = torch.empty(P, dtype=torch.float32, device="cuda")
+        gpu.mix_seq(out, _dev(local), [_dev(x) for x in nbrs], alphas)
+        assert np.array_equal(out.cpu().numpy(), ref), (n, P)
+
+
+def test_mix_seq_varied_alphas_and_inplace(gpu):
+    rng = np.random.default_rng(7)
+    P = 1_000_003
+    local = _rand(rng, 1, P)[0]
+    nbrs = _rand(rng, 5, P)
+    alphas = [0.1, 0.5, 1.0, 0.3333333, 0.9]
+    ref = O.sequential_mix(local, nbrs, alphas)
+    w = _dev(local)
+    gpu.mix_seq(w, w, [_dev(x) for x in nbrs], alphas)  # out aliases local
+    assert np.array_equal(w.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("offsets", [(1, 1, 1), (2, 2, 2), (3, 3, 3), (0, 1, 2), (1, 0, 3)])
+def test_mix_seq_misaligned_views(gpu, offsets):
+    """Sub-tensor views at element offsets: same misalignment -> scalar head + float4 body,
+    mixed misalignment -> scalar path. Results identical either way."""
+    rng = np.random.default_rng(11)
+    P = 100_003
+    base = [_dev(np.zeros(P + 8, np.float32)) for _ in range(3)]
+    local = _rand(rng, 1, P)[0]
+    nbrs = _rand(rng, 2, P)
+    o_out, o_loc, o_nb = offsets
+    out = base[0][o_out:o_out + P]
+    loc = base[1][o_loc:o_loc + P]
+    loc.copy_(_dev(local))
+    nb0 = base[2][o_nb:o_nb + P]
+    nb0.copy_(_dev(nbrs[0]))
+    gpu.mix_seq(out, loc, [nb0, _dev(nbrs[1])], [1 / 3, 1 / 3])
+    assert np.array_equal(out.cpu().numpy(), O.sequential_mix(local, nbrs, [1 / 3, 1 / 3]))
+
+
+@pytest.mark.parametrize("n", [1, 3, 8, 20])
+def test_mix_linear_closed_form(gpu, n):
+    rng = np.random.default_rng(200 + n)
+    P = 2_000_001
+    local = _rand(rng, 1, P)[0]
+    nbrs = _rand(rng, n, P)
+    alphas = [1.0 / (n + 1)] * n
+    coeff = O.closed_form_coeffs(alphas)
+    out = torch.empty(P, dtype=torch.float32, device="cuda")
+    gpu.mix_linear(out, _dev(local), [_dev(x) for x in nbrs], coeff)
+    ref = O.sequential_mix(local.astype(np.float64), [x.astype(np.float64) for x in nbrs], alphas)
+    assert normwise_close(out.cpu().numpy(), ref)
+
+
+def test_mix_strided_gradient_slices(gpu):
+    """[..., devices] gradient layout (cfa_ge_2stage.py:594-606): slot ii read with stride D."""
+    rng = np.random.default_rng(5)
+    P, D, ii = 50_000, 16, 7
+    local = _rand(rng, 1, P)[0]
+    stacks = [rng.standard_normal((P, D)).astype(np.float32) for _ in range(3)]
+    alphas = [0.25, 0.5, 0.125]
+    ref = O.sequential_mix(local, [s[:, ii].copy() for s in stacks], alphas)
+    dstacks = [_dev(s) for s in stacks]
+    out = torch.empty(P, dtype=torch.float32, device="cuda")
+    gpu.mix_strided(out, _dev(local), [s[:, ii] for s in dstacks], alphas)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def _compress_expect(local, nbrs, alphas, mode, cb, ce):
+    y = O.sequential_mix(local, nbrs, alphas).astype(np.float32)
+    seg = y[cb:ce].astype(np.float64)
+    cnt = O.tf1_compress(seg, local[cb:ce].astype(np.float64), mode)
+    y = y.copy()
+    y[cb:ce] = seg.astype(np.float32)
+    return y, cnt
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n", [0, 1, 3, 17])
+def test_mix_seq_compress(gpu, mode, n):
+    rng = np.random.default_rng(300 + 10 * mode + n)
+    P = 24_622  # FL_CFA_CNN_tf2 bucket; W2 = [40, 24616)
+    cb, ce = 40, 40 + 24_576
+    base = (rng.standard_normal(P) * 0.01).astype(np.float32)
+    local = base + (rng.standard_normal(P) * 3e-4).astype(np.float32)
+    nbrs = [base + (rng.standard_normal(P) * 3e-4).astype(np.float32) for _ in range(n)]
+    alphas = [1.0 / (n + 1)] * n
+    ref, cnt = _compress_expect(local, nbrs, alphas, mode, cb, ce)
+    out = torch.empty(P, dtype=torch.float32, device="cuda")
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.mix_seq_compress(out, _dev(local), [_dev(x) for x in nbrs], alphas, mode, cb, ce, kept)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert int(kept.item()) == cnt
+    if mode in (1, 4) or (mode and n):
+        assert 0 < cnt < ce - cb  # the regime exercises both branches
+    elif mode:
+        assert cnt == 0  # DPCM with no neighbour: y == ref everywhere (cfa_ongraphs.py:218-249)
+
+
+@pytest.mark.parametrize("filtered,init", [(True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_mewma_bitexact_fp32(gpu, filtered, init, n):
+    rng = np.random.default_rng(400 + n)
+    P, split = 1488 * 37 + 3, 136 * 37
+    rho, lr1, lr2 = 0.99, 0.1, 0.05
+    W = _rand(rng, 1, P)[0]
+    s = _rand(rng, n, P)
+    g = _rand(rng, n, P)
+    # fp32 oracle: same op order as cfa_ge_2stage.py:594-621 on fp32 arrays
+    Wr, sr = W.copy(), [x.copy() for x in s]
+    lr = np.where(np.arange(P) < split, np.float32(lr1), np.float32(lr2)).astype(np.float32)
+    for j in range(n):
+        sr[j] = g[j].copy() if init else rho * g[j] + (1 - rho) * sr[j]
+        Wr = Wr - lr * (sr[j] if filtered else g[j])
+    dW, ds = _dev(W), [_dev(x) for x in s]
+    gpu.mewma(dW, ds, [_dev(x) for x in g], rho, lr1, lr2, split, init, filtered)
+    assert np.array_equal(dW.cpu().numpy(), Wr)
+    for j in range(n):
+        assert np.array_equal(ds[j].cpu().numpy(), sr[j])
+
+
+def test_population_kernel_matches_per_device(gpu):
+    """One launch over a k-regular population == per-device sequential mixes."""
+    rng = np.random.default_rng(9)
+    D, P, N = 12, 100_001, 4
+    buckets = _rand(rng, D, P)
+    dev = [_dev(b) for b in buckets]
+    outs = [torch.empty(P, dtype=torch.float32, device="cuda") for _ in range(D)]
+    ptr, idx, coef = [0], [], []
+    expect = []
+    for d in range(D):
+        nbr = O.tf1_kregular(d, N, D).tolist()
+        a = 1.0 / (len(nbr) + 1)
+        idx += [d] + nbr
+        coef += [1.0] + [a] * len(nbr)
+        ptr.append(len(idx))
+        expect.append(O.sequential_mix(buckets[d], [buckets[j] for j in nbr], [a] * len(nbr)))
+    t64 = lambda xs: torch.tensor([x.data_ptr() for x in xs], dtype=torch.int64, device="cuda")
+    gpu.population(t64(outs), t64(dev), torch.tensor(ptr, dtype=torch.int32, device="cuda"),
+                   torch.tensor(idx, dtype=torch.int32, device="cuda"),
+                   torch.tensor(coef, dtype=torch.float32, device="cuda"), D, 0, P)
+    for d in range(D):
+        assert np.array_equal(outs[d].cpu().numpy(), expect[d]), d
+
+
+def test_full_size_properties(gpu):
+    """BASELINE size (8 neighbours x 25M fp32): exact against the oracle on a sampled window,
+    plus size-independent properties (identity at a=0, convexity bound)."""
+    P, n = 25_000_000, 8
+    g = torch.Generator(device="cuda").manual_seed(20261015)
+    local = torch.randn(P, generator=g, device="cuda")
+    nbrs = [torch.randn(P, generator=g, device="cuda") for _ in range(n)]
+    out = torch.empty_like(local)
+    a = 1.0 / (n + 1)
+    gpu.mix_seq(out, local, nbrs, [a] * n)
+    lo = torch.minimum(local, torch.stack(nbrs).min(0).values)
+    hi = torch.maximum(local, torch.stack(nbrs).max(0).values)
+    assert bool(((out >= lo - 1e-6) & (out <= hi + 1e-6)).all())
+    sl = slice(12_345_678, 12_345_678 + 65_536)
+    ref = O.sequential_mix(local[sl].cpu().numpy(), [x[sl].cpu().numpy() for x in nbrs], [a] * n)
+    assert np.array_equal(out[sl].cpu().numpy(), ref)
+    gpu.mix_seq(out, local, nbrs[:1], [0.0])
+    assert torch.equal(out, local)
+
+
+def test_error_paths(gpu):
+    from federated_amd import _lib
+    x = torch.zeros(16, device="cuda")
+    with pytest.raises(_lib.CFAError, match="aliases neighbour"):
+        gpu.mix_seq(x, torch.zeros(16, device="cuda"), [x], [0.5])
+    with pytest.raises(ValueError):
+        gpu.mix_seq(x, torch.zeros(8, device="cuda"), [], [])
+    with pytest.raises(TypeError):
+        gpu.mix_seq(x, torch.zeros(16, device="cuda", dtype=torch.float64), [], [])
