@@ -50,6 +50,8 @@ SIGNATURES = {
     "cfa_version": (_c_int, []),
     "cfa_last_error": (ctypes.c_char_p, []),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
+    "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
+                                    _c_void_p, _c_void_p]),
     "cfa_mix_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_strided_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_int64_p, _c_float_p, _c_int,
                                      _c_size_t, _c_void_p]),
@@ -70,6 +72,12 @@ SIGNATURES = {
     "cfa_allreduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
 }
+
+class Launch(ctypes.Structure):
+    """cfa_launch_t"""
+    _fields_ = [("blocks_per_cu", ctypes.c_int), ("vec_per_lane", ctypes.c_int),
+                ("nontemporal", ctypes.c_int)]
+
 
 _lock = threading.Lock()
 _lib = None

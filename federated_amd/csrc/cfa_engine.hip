@@ -70,22 +70,19 @@ namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
-// Launch tuning, read once from the environment (immutable after first use).
-struct Tune {
-  int blocks_per_cu;  // grid = min(tiles, CUs * blocks_per_cu); 0 = one block per tile
-  int unroll;         // 16-byte vectors per lane per stream per tile (1 or 2)
-  int nontemporal;    // 1 = nontemporal loads/stores for the once-read streams
-};
-
-static Tune read_tune() {
-  Tune t{0, 2, 1};
+// Default launch configuration (cfa_launch_t), optionally overridden once from the
+// environment (CFA_BLOCKS_PER_CU, CFA_VEC_PER_LANE, CFA_NONTEMPORAL); immutable after first use.
+// Explicit per-call configurations go through cfa_mix_seq_ex_f32.
+static int norm_vec(int v) { return v >= 4 ? 4 : (v >= 2 ? 2 : 1); }
+static cfa_launch_t read_tune() {
+  cfa_launch_t t{0, 2, 1};
   if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
-  if (const char* s = getenv("CFA_UNROLL")) t.unroll = atoi(s) >= 2 ? 2 : 1;
+  if (const char* s = getenv("CFA_VEC_PER_LANE")) t.vec_per_lane = norm_vec(atoi(s));
   if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
   return t;
 }
-static const Tune& tune() {
-  static const Tune t = read_tune();  // C++11 magic static: thread-safe init
+static const cfa_launch_t& tune() {
+  static const cfa_launch_t t = read_tune();  // C++11 magic static: thread-safe init
   return t;
 }
 
@@ -99,9 +96,8 @@ static int device_cus() {
   return cus;
 }
 
-static unsigned grid_for(long long tiles) {
+static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
   if (tiles <= 0) return 1;
-  const Tune& t = tune();
   long long g = tiles;
   if (t.blocks_per_cu > 0) {
     long long cap = (long long)device_cus() * t.blocks_per_cu;
@@ -461,12 +457,15 @@ static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const
 }
 
 template <int RULE>
-static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec) {
-  const Tune& t = tune();
-  const int U = t.unroll;
+static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                       const cfa_launch_t& t) {
+  const int U = norm_vec(t.vec_per_lane);
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
-  const unsigned grid = grid_for(tiles);
-  if (U == 2) {
+  const unsigned grid = grid_for(tiles, t);
+  if (U == 4) {
+    if (t.nontemporal) launch_vec_u<RULE, 4, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 4, false>(n, grid, st, out, f, nvec);
+  } else if (U == 2) {
     if (t.nontemporal) launch_vec_u<RULE, 2, true>(n, grid, st, out, f, nvec);
     else launch_vec_u<RULE, 2, false>(n, grid, st, out, f, nvec);
   } else {
@@ -510,7 +509,8 @@ static int compress_params(int mode, CompressParams& cp) {
 // every pointer is 16-byte aligned, when they share the same misalignment), a float4 body and
 // a scalar tail. Buckets with different misalignments run entirely on the scalar path.
 static int mix_pass(float* out, const float* local, const float* const* nbrs, const float* c,
-                    int n, size_t P, int rule, const CompressParams* cp, hipStream_t st) {
+                    int n, size_t P, int rule, const CompressParams* cp, hipStream_t st,
+                    const cfa_launch_t& lc = tune()) {
   const uintptr_t mis = addr(out) & 15;
   bool same = (addr(local) & 15) == mis;
   for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
@@ -539,9 +539,9 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
       shifted.cend = cpv.cend - (long long)head;
       launch_vec_compress(n, st, out + head, f, (long long)nvec, shifted);
     } else if (rule == CFA_RULE_SEQUENTIAL) {
-      launch_vec<CFA_RULE_SEQUENTIAL>(n, st, out + head, f, (long long)nvec);
+      launch_vec<CFA_RULE_SEQUENTIAL>(n, st, out + head, f, (long long)nvec, lc);
     } else {
-      launch_vec<CFA_RULE_LINEAR>(n, st, out + head, f, (long long)nvec);
+      launch_vec<CFA_RULE_LINEAR>(n, st, out + head, f, (long long)nvec, lc);
     }
     if (int rc = check_launch("mix_vec")) return rc;
   }
@@ -591,7 +591,7 @@ static bool needs_ref(int mode) {
 }
 static int mix_seq_any(float* out, const float* local, const float* const* nbrs,
                        const float* alphas, int n, size_t P, const CompressParams* cp,
-                       hipStream_t st) {
+                       hipStream_t st, const cfa_launch_t& lc = tune()) {
   if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
   if (P == 0) return CFA_OK;
   const bool split_epilogue = cp && n > CFA_MAX_FANIN;
@@ -605,7 +605,8 @@ static int mix_seq_any(float* out, const float* local, const float* const* nbrs,
     c[0] = 1.0f;
     for (int j = 0; j < m; ++j) c[j + 1] = alphas[done + j];
     const CompressParams* fused = (cp && !split_epilogue) ? cp : nullptr;
-    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL, fused, st)) return rc;
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL, fused, st, lc))
+      return rc;
     done += m;
     w = out;
   } while (done < n);
@@ -624,6 +625,16 @@ extern "C" int cfa_mix_seq_f32(float* out, const float* local, const float* cons
                                const float* alphas, int n, size_t P, void* stream) {
   if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
   return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int cfa_mix_seq_ex_f32(float* out, const float* local, const float* const* nbrs,
+                                  const float* alphas, int n, size_t P,
+                                  const cfa_launch_t* launch, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  cfa_launch_t lc = launch ? *launch : tune();
+  if (lc.blocks_per_cu < 0) return fail(CFA_E_INVALID, "blocks_per_cu < 0");
+  lc.vec_per_lane = norm_vec(lc.vec_per_lane);
+  return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream, lc);
 }
 
 extern "C" int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,

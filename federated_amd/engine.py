@@ -10,6 +10,7 @@ reference's per-layer arrays to and from that flat form.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Iterable, Optional, Sequence
 
 import numpy as np
@@ -106,17 +107,24 @@ class Engine:
 
     # -- mixing ----------------------------------------------------------------------------
     def mix_seq(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
-                alphas: Sequence[float], stream=None) -> torch.Tensor:
-        """out = fold_j(w <- w + alphas[j]*(nbrs[j] - w)), w0 = local (sequential CFA rule)."""
+                alphas: Sequence[float], stream=None, launch: Optional[tuple] = None) -> torch.Tensor:
+        """out = fold_j(w <- w + alphas[j]*(nbrs[j] - w)), w0 = local (sequential CFA rule).
+        ``launch`` = (blocks_per_cu, vec_per_lane, nontemporal) overrides the launch shape."""
         P = _check_bucket(local, "local")
         _check_bucket(out, "out", P)
         for j, x in enumerate(nbrs):
             _check_bucket(x, f"nbrs[{j}]", P)
         if len(alphas) != len(nbrs):
             raise ValueError("one alpha per neighbour required")
-        _lib.call("cfa_mix_seq_f32", out.data_ptr(), local.data_ptr(),
-                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(alphas),
-                  len(nbrs), P, self.stream_handle(stream))
+        table = _lib.ptr_table([x.data_ptr() for x in nbrs])
+        if launch is None:
+            _lib.call("cfa_mix_seq_f32", out.data_ptr(), local.data_ptr(), table,
+                      _lib.float_array(alphas), len(nbrs), P, self.stream_handle(stream))
+        else:
+            lc = _lib.Launch(*launch)
+            _lib.call("cfa_mix_seq_ex_f32", out.data_ptr(), local.data_ptr(), table,
+                      _lib.float_array(alphas), len(nbrs), P, ctypes.addressof(lc),
+                      self.stream_handle(stream))
         return out
 
     def mix_linear(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],

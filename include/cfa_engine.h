@@ -86,6 +86,19 @@ CFA_API const char* cfa_last_error(void);
 CFA_API int cfa_mix_seq_f32(float* out, const float* local, const float* const* nbrs,
                     const float* alphas, int n, size_t P, void* stream);
 
+/* Launch configuration of the streaming mix kernels (performance only; results are identical
+ * for every configuration). */
+typedef struct {
+  int blocks_per_cu;  /* grid = min(tiles, CUs * blocks_per_cu); 0 = one workgroup per tile */
+  int vec_per_lane;   /* 16-byte vectors per lane per bucket per tile: 1, 2 or 4 */
+  int nontemporal;    /* 1 = nontemporal (streaming) loads/stores for once-touched buckets */
+} cfa_launch_t;
+
+/* cfa_mix_seq_f32 with an explicit launch configuration (NULL = library default). */
+CFA_API int cfa_mix_seq_ex_f32(float* out, const float* local, const float* const* nbrs,
+                               const float* alphas, int n, size_t P, const cfa_launch_t* launch,
+                               void* stream);
+
 /* Linear-combination mix: out[i] = coeff[0]*local[i] + sum_j coeff[j+1]*nbrs[j][i].
  * The closed form of the sequential rule (c_0 = prod(1-a_j), c_{j+1} = a_j prod_{k>j}(1-a_k)),
  * and the FedAvg / parameter-server aggregation shape

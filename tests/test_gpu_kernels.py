@@ -98,8 +98,9 @@ def test_mix_strided_gradient_slices(gpu):
 
 def _compress_expect(local, nbrs, alphas, mode, cb, ce):
     y = O.sequential_mix(local, nbrs, alphas).astype(np.float32)
-    seg = y[cb:ce].astype(np.float64)
-    cnt = O.tf1_compress(seg, local[cb:ce].astype(np.float64), mode)
+    seg = y[cb:ce].astype(np.float64).reshape(-1, 6)  # W2 is [4096, 6]
+    cnt = O.tf1_compress(seg, local[cb:ce].astype(np.float64).reshape(-1, 6), mode)
+    seg = seg.reshape(-1)
     y = y.copy()
     y[cb:ce] = seg.astype(np.float32)
     return y, cnt
