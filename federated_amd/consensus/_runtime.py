@@ -1,0 +1,164 @@
+"""Shared runtime of the drop-in ``consensus`` modules.
+
+* The reference's exchange protocol: polling for neighbour files with ``pause(1)``, one retry
+  after ``pause(3)`` when a load fails, and the fixed protocol sleeps (``pause(2)``/``pause(5)``
+  around each neighbour). ``pause`` here sleeps ``seconds * FEDERATED_AMD_PAUSE_SCALE``
+  (default 1.0 = the reference's timing; set 0 to drop the protocol sleeps).
+* ``HostMixer``: the host-array front end of the GPU engine. Per call it flattens the caller's
+  per-layer arrays into one bucket (layer order kept), copies the local and the n neighbour
+  buckets to HBM, runs ONE libcfa kernel that folds all n neighbours (plus the optional fused
+  compression epilogue), and copies the result back. There is no CPU fallback: without a GPU
+  the engine raises.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.io as sio
+import torch
+
+from ..engine import BucketLayout, get_engine
+
+
+def _scale() -> float:
+    try:
+        return float(os.environ.get("FEDERATED_AMD_PAUSE_SCALE", "1"))
+    except ValueError:
+        return 1.0
+
+
+def pause(seconds: float) -> None:
+    """matplotlib.pyplot.pause(seconds) as the reference uses it: a protocol sleep."""
+    s = float(seconds) * _scale()
+    if s > 0:
+        time.sleep(s)
+
+
+def wait_for(*paths: str) -> float:
+    """Poll until every path exists (cfa.py:120-124: ``pause(1)`` between checks). Returns the
+    time spent waiting."""
+    t0 = time.time()
+    while not all(os.path.isfile(p) for p in paths):
+        pause(1)
+        if _scale() == 0:
+            time.sleep(0.01)
+    return time.time() - t0
+
+
+def loadmat_retry(path: str) -> dict:
+    """sio.loadmat with the reference's single retry after pause(3) (cfa.py:43-48)."""
+    try:
+        return sio.loadmat(path)
+    except Exception:
+        print("Detected problem while loading file")
+        pause(3)
+        return sio.loadmat(path)
+
+
+def savemat_retry(path: str, data: dict) -> None:
+    """sio.savemat with the reference's single retry after pause(3) (cfa.py:131-139)."""
+    try:
+        sio.savemat(path, data)
+    except Exception:
+        print("Unable to save file .. retrying")
+        pause(3)
+        sio.savemat(path, data)
+
+
+class HostMixer:
+    """Host arrays in, host arrays out; the arithmetic runs in libcfa on the GPU."""
+
+    def __init__(self, device=None):
+        self.engine = get_engine(device)
+        self._tls = threading.local()
+
+    def _stream(self) -> torch.cuda.Stream:
+        s = getattr(self._tls, "stream", None)
+        if s is None:
+            s = self._tls.stream = torch.cuda.Stream(self.engine.device)
+        return s
+
+    def _upload(self, layout: BucketLayout, arrays) -> torch.Tensor:
+        host = torch.from_numpy(layout.pack(arrays))
+        return host.to(self.engine.device, non_blocking=False)
+
+    def mix(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float],
+            compress: Optional[Tuple[int, int]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
+        """Sequential CFA mix of the per-layer arrays ``local`` with each neighbour's per-layer
+        arrays, w <- w + alphas[j] * (x_j - w) per layer, all n neighbours folded in one kernel.
+        ``compress=(mode, layer)`` fuses the cfa_ongraphs compression epilogue on that layer
+        (with the pre-mix local as DPCM reference) and returns the kept count.
+        Returns (fp32 arrays with the local shapes, kept count or None)."""
+        layout = BucketLayout.of(local)
+        with torch.cuda.stream(self._stream()):
+            d_local = self._upload(layout, local)
+            d_nbrs = [self._upload(layout, x) for x in nbrs]
+            out = torch.empty_like(d_local)
+            kept = None
+            if compress is not None:
+                mode, layer = compress
+                b, e = layout.segment(layer)
+                kept = self.engine.counter()
+                self.engine.mix_seq_compress(out, d_local, d_nbrs, list(alphas), mode, b, e, kept,
+                                             stream=self._stream())
+            else:
+                self.engine.mix_seq(out, d_local, d_nbrs, list(alphas), stream=self._stream())
+            flat = out.cpu().numpy()
+            kept_n = int(kept.item()) if kept is not None else None
+        return layout.unpack(flat, copy=False), kept_n
+
+    def compress(self, y: np.ndarray, ref: Optional[np.ndarray], mode: int) -> Tuple[np.ndarray, int]:
+        """Standalone compression epilogue (cfa_ongraphs.py:225-273) on one tensor."""
+        layout = BucketLayout([np.shape(y)])
+        with torch.cuda.stream(self._stream()):
+            dy = self._upload(layout, [y])
+            dr = self._upload(layout, [ref]) if ref is not None else None
+            kept = self.engine.counter()
+            self.engine.compress(dy, dr, mode, kept, stream=self._stream())
+            flat = dy.cpu().numpy()
+            n = int(kept.item())
+        return flat.reshape(np.shape(y)), n
+
+    def mewma(self, W: Sequence, states: Sequence[np.ndarray], grads: Sequence[Sequence], rho: float,
+              lrs: Sequence[float], init: bool, use_filtered: bool) -> List[np.ndarray]:
+        """CFA-GE update of the per-layer model ``W`` with the neighbours' slot gradients
+        ``grads[j]`` (per-layer arrays) and the per-layer saved-state arrays ``states[k]`` of shape
+        [..., N] (updated IN PLACE at slot j, as the reference does). ``lrs`` = per-layer learning
+        rate; layers with the first rate must precede the others (layer 1 then layer 2)."""
+        layout = BucketLayout.of(W)
+        n = len(grads)
+        first_other = next((k for k in range(len(lrs)) if lrs[k] != lrs[0]), len(lrs))
+        if any(lr != lrs[-1] for lr in lrs[first_other:]):
+            raise ValueError("learning rates must be one value for the leading layers, one for the rest")
+        split = int(layout.offsets[first_other])
+        lr1, lr2 = float(lrs[0]), float(lrs[-1])
+        with torch.cuda.stream(self._stream()):
+            dW = self._upload(layout, W)
+            ds = [self._upload(layout, [np.asarray(st)[..., j] for st in states]) for j in range(n)]
+            dg = [self._upload(layout, g) for g in grads]
+            self.engine.mewma(dW, ds, dg, rho, lr1, lr2, split, init, use_filtered,
+                              stream=self._stream())
+            W_out = dW.cpu().numpy()
+            s_out = [x.cpu().numpy() for x in ds]
+        for j in range(n):
+            for k, arr in enumerate(layout.unpack(s_out[j], copy=False)):
+                states[k][..., j] = arr
+        return layout.unpack(W_out, copy=False)
+
+
+_mixers = {}
+_mlock = threading.Lock()
+
+
+def mixer() -> HostMixer:
+    """Process-wide HostMixer on the current GPU (created on first use)."""
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+    with _mlock:
+        m = _mixers.get(dev)
+        if m is None:
+            m = _mixers[dev] = HostMixer(dev)
+    return m

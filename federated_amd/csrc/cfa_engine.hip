@@ -73,9 +73,13 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // Default launch configuration (cfa_launch_t), optionally overridden once from the
 // environment (CFA_BLOCKS_PER_CU, CFA_VEC_PER_LANE, CFA_NONTEMPORAL); immutable after first use.
 // Explicit per-call configurations go through cfa_mix_seq_ex_f32.
-static int norm_vec(int v) { return v >= 4 ? 4 : (v >= 2 ? 2 : 1); }
+// Defaults from the in-process sweep on MI355X (tools/tune_mix.py, profiles/r01_tune.jsonl):
+// 2 resident workgroups per CU with a grid-stride loop, nontemporal loads and stores, and
+// vec_per_lane = 0 (auto: the widest tile that keeps (n+1)*vec <= 40 float4 in registers).
+static int norm_vec(int v) { return v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0)); }
+static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ? 2 : 1); }
 static cfa_launch_t read_tune() {
-  cfa_launch_t t{0, 2, 1};
+  cfa_launch_t t{2, 0, 1};
   if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
   if (const char* s = getenv("CFA_VEC_PER_LANE")) t.vec_per_lane = norm_vec(atoi(s));
   if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
@@ -459,7 +463,7 @@ static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const
 template <int RULE>
 static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
                        const cfa_launch_t& t) {
-  const int U = norm_vec(t.vec_per_lane);
+  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : auto_vec(n);
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   const unsigned grid = grid_for(tiles, t);
   if (U == 4) {

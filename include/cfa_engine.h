@@ -90,7 +90,7 @@ CFA_API int cfa_mix_seq_f32(float* out, const float* local, const float* const* 
  * for every configuration). */
 typedef struct {
   int blocks_per_cu;  /* grid = min(tiles, CUs * blocks_per_cu); 0 = one workgroup per tile */
-  int vec_per_lane;   /* 16-byte vectors per lane per bucket per tile: 1, 2 or 4 */
+  int vec_per_lane;   /* 16-byte vectors per lane per bucket per tile: 1, 2, 4; 0 = auto */
   int nontemporal;    /* 1 = nontemporal (streaming) loads/stores for once-touched buckets */
 } cfa_launch_t;
 

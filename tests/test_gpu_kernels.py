@@ -122,9 +122,9 @@ def test_mix_seq_compress(gpu, mode, n):
     gpu.mix_seq_compress(out, _dev(local), [_dev(x) for x in nbrs], alphas, mode, cb, ce, kept)
     assert np.array_equal(out.cpu().numpy(), ref)
     assert int(kept.item()) == cnt
-    if mode in (1, 4) or (mode and n):
+    if mode in (1, 2, 4) and (n or mode in (1, 4)):
         assert 0 < cnt < ce - cb  # the regime exercises both branches
-    elif mode:
+    elif mode in (2, 3) and not n:
         assert cnt == 0  # DPCM with no neighbour: y == ref everywhere (cfa_ongraphs.py:218-249)
 
 

@@ -31,7 +31,7 @@ def main():
         xs = [torch.randn(P, device="cuda") for _ in range(K + 1)]
         sets.append((xs[0], xs[1:], torch.empty(P, device="cuda")))
     alphas = [1.0 / (K + 1)] * K
-    cfgs = list(itertools.product([0, 2, 4, 8, 16], [1, 2, 4], [0, 1]))
+    cfgs = list(itertools.product([0, 1, 2, 3, 4, 8], [0, 1, 2, 4], [0, 1]))
     times = {c: [] for c in cfgs}
     ref = torch.empty(P, device="cuda")
     eng.mix_seq(ref, sets[0][0], sets[0][1], alphas)
