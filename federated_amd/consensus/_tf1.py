@@ -103,10 +103,12 @@ def gpu_mix(local4: Sequence, nbr_models: Sequence, alphas: Sequence[float], com
     return mixer().mix(list(local4), nbr_models, alphas, compress)
 
 
-def publish(ii: int, epoch: int, W1, b1, W2, b2, **extra) -> None:
+def publish(dev: int, ep: int, W1, b1, W2, b2, **extra) -> None:
+    """Write datamat{dev}_{ep}.mat with the four tensors plus any extra keys (epoch,
+    loss_sample, counter_param), as the reference's savemat calls do."""
     data = {"weights1": W1, "biases1": b1, "weights2": W2, "biases2": b2}
     data.update(extra)
-    savemat_retry("datamat{}_{}.mat".format(ii, epoch), data)
+    savemat_retry("datamat{}_{}.mat".format(dev, ep), data)
 
 
 def squeeze_out(W1, b1, W2, b2):
