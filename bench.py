@@ -98,6 +98,36 @@ def load_traffic(path: str, P: int, K: int):
     return None
 
 
+def open_transport(kind, rank, world, device):
+    """The requested transport; if it cannot be opened, torch.distributed P2P over an nccl
+    (= RCCL) group, then over the gloo group (host-staged) as the last resort. The transport
+    used is reported in the JSON config."""
+    import torch.distributed as dist
+    from federated_amd.dist import TorchTransport, make_transport
+    import torch
+    t, ok = None, 1
+    try:
+        t = make_transport(kind, rank, world, device)
+    except Exception as exc:
+        ok = 0
+        print(f"[bench rank {rank}] {kind} transport failed ({exc})", file=sys.stderr)
+    flag = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank takes the same decision
+    if int(flag.item()) == 1:
+        return t
+    if t is not None:
+        t.close()
+    try:
+        t = TorchTransport(dist.new_group(backend="nccl"))
+        t.name = "torch-nccl"
+        return t
+    except Exception as exc:
+        print(f"[bench rank {rank}] torch nccl group failed ({exc}); using gloo", file=sys.stderr)
+    t = TorchTransport()
+    t.name = "torch-gloo"
+    return t
+
+
 def main():
     args = parse()
     import torch
@@ -109,21 +139,26 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        sys.exit("bench.py needs a ROCm GPU")
+    device = local_rank % ndev  # one rank per GPU; more ranks than GPUs only for rehearsal (torch transport)
+    torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from federated_amd.engine import get_engine
     from federated_amd.population import RingPopulationShard, RingShardPlan
-    from federated_amd.dist import make_transport
 
     P, K, L = args.params, args.neighbours, args.devices_per_gpu
     if K % 2:
         sys.exit("--neighbours must be even (ring window K/2 per side)")
-    eng = get_engine(local_rank)
+    eng = get_engine(device)
     plan = RingShardPlan(rank, world, L, K // 2)
-    transport = make_transport(args.transport, rank, world, local_rank) if world > 1 else None
-    shard = RingPopulationShard(plan, P, torch.device("cuda", local_rank), transport, eng)
+    transport = None
+    if world > 1:
+        transport = open_transport(args.transport, rank, world, device)
+    shard = RingPopulationShard(plan, P, torch.device("cuda", device), transport, eng)
 
     gen = torch.Generator(device=shard.device)
     for i in range(L):  # synthetic models: seeded per global device id

@@ -16,6 +16,7 @@ Two interchangeable transports:
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import List, Optional, Sequence, Tuple
 
@@ -34,15 +35,27 @@ class TorchTransport:
         self.group = group
 
     def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
-        ops = []
-        for buf, peer in sends:
-            ops.append(dist.P2POp(dist.isend, buf, peer, group=self.group))
-        for buf, peer in recvs:
-            ops.append(dist.P2POp(dist.irecv, buf, peer, group=self.group))
-        if not ops:
+        """Grouped exchange. gloo moves host tensors only, so device buffers are staged through
+        host memory (synchronously); with nccl the ops are issued on ``stream``."""
+        if not sends and not recvs:
             return
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        staged = dist.get_backend(self.group) == "gloo"
+        if staged:
+            if stream is not None and any(b.is_cuda for b, _ in list(sends) + list(recvs)):
+                stream.synchronize()
+            s_bufs = [(b.cpu() if b.is_cuda else b, p) for b, p in sends]
+            r_bufs = [(torch.empty(b.shape, dtype=b.dtype) if b.is_cuda else b, p) for b, p in recvs]
+        else:
+            s_bufs, r_bufs = list(sends), list(recvs)
+        ctx = torch.cuda.stream(stream) if (stream is not None and not staged) else contextlib.nullcontext()
+        with ctx:
+            ops = [dist.P2POp(dist.isend, b, p, group=self.group) for b, p in s_bufs]
+            ops += [dist.P2POp(dist.irecv, b, p, group=self.group) for b, p in r_bufs]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for (dst, _), (src, _) in zip(recvs, r_bufs):
+            if dst is not src:
+                dst.copy_(src)
 
     def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
@@ -60,11 +73,17 @@ class RcclTransport:
         from . import _lib
         self._lib = _lib
         uid = (ctypes.c_char * _lib.CFA_UNIQUE_ID_BYTES)()
+        payload = [None]
         if rank == 0:
-            _lib.call("cfa_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
-        payload = [bytes(uid) if rank == 0 else None]
-        if world > 1:
+            try:
+                _lib.call("cfa_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
+                payload = [bytes(uid)]
+            except _lib.CFAError as exc:
+                payload = [f"error: {exc}"]
+        if world > 1:  # rank 0 always broadcasts (id or failure), so no rank is left waiting
             dist.broadcast_object_list(payload, src=0, group=group)
+        if not isinstance(payload[0], bytes):
+            raise RuntimeError(f"RCCL unique id unavailable ({payload[0]})")
         ctypes.memmove(uid, payload[0], _lib.CFA_UNIQUE_ID_BYTES)
         comm = ctypes.c_void_p()
         _lib.call("cfa_comm_init", ctypes.byref(comm), rank, world, ctypes.cast(uid, ctypes.c_void_p),
