@@ -30,6 +30,7 @@ CFA_UNIQUE_ID_BYTES = 128
 
 RULE_SEQUENTIAL = 0
 RULE_LINEAR = 1
+RULE_SEQUENTIAL_DIV = 2
 
 COMPRESS_NONE = 0
 COMPRESS_SPARSE = 1
@@ -52,6 +53,8 @@ SIGNATURES = {
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
                                     _c_void_p, _c_void_p]),
+    "cfa_mix_seq_div_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_float_p, _c_int,
+                                     _c_size_t, _c_void_p]),
     "cfa_mix_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_strided_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_int64_p, _c_float_p, _c_int,
                                      _c_size_t, _c_void_p]),

@@ -16,12 +16,15 @@ first and alias the package).
 import importlib
 import sys
 
-_TF1 = ("cfa", "cfa_mobilenet", "cfa_ongraphs", "cfa_ge_2stage", "cfa_ge_4stage")
-_TF2 = ("consensus_v2", "consensus_v3", "consensus_v3_threading", "consensus_v4")
+_TF1 = ("cfa", "cfa_mobilenet", "cfa_ongraphs", "cfa_ge_2stage", "cfa_ge_4stage", "cfa_ge_2stage_mobilenet")
+_TF2 = ("consensus_v2", "consensus_v3", "consensus_v3_threading", "consensus_v4", "parameter_server",
+        "parameter_server_v2")
 _VARIANTS = {
     None: {},
-    "fl_radar": {"consensus_v3": "fl_radar.consensus_v3", "consensus_v4": "fl_radar.consensus_v4"},
-    "fl_over_mqtt": {"consensus_v3": "fl_over_mqtt.consensus_v3"},
+    "fl_radar": {"consensus_v3": "fl_radar.consensus_v3", "consensus_v4": "fl_radar.consensus_v4",
+                 "parameter_server": "parameter_server_099"},
+    "fl_over_mqtt": {"consensus_v3": "fl_over_mqtt.consensus_v3", "parameter_server": "parameter_server_099"},
+    "cifar100": {"parameter_server": "parameter_server_099"},
 }
 
 

@@ -87,11 +87,13 @@ class HostMixer:
         return host.to(self.engine.device, non_blocking=False)
 
     def mix(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float],
-            compress: Optional[Tuple[int, int]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
+            compress: Optional[Tuple[int, int]] = None,
+            divisors: Optional[Sequence[float]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
         """Sequential CFA mix of the per-layer arrays ``local`` with each neighbour's per-layer
         arrays, w <- w + alphas[j] * (x_j - w) per layer, all n neighbours folded in one kernel.
         ``compress=(mode, layer)`` fuses the cfa_ongraphs compression epilogue on that layer
         (with the pre-mix local as DPCM reference) and returns the kept count.
+        ``divisors`` selects the FedAvg form w <- w + (alphas[j] * (x_j - w)) / divisors[j].
         Returns (fp32 arrays with the local shapes, kept count or None)."""
         layout = BucketLayout.of(local)
         with torch.cuda.stream(self._stream()):
@@ -105,6 +107,9 @@ class HostMixer:
                 kept = self.engine.counter()
                 self.engine.mix_seq_compress(out, d_local, d_nbrs, list(alphas), mode, b, e, kept,
                                              stream=self._stream())
+            elif divisors is not None:
+                self.engine.mix_seq_div(out, d_local, d_nbrs, list(alphas), list(divisors),
+                                        stream=self._stream())
             else:
                 self.engine.mix_seq(out, d_local, d_nbrs, list(alphas), stream=self._stream())
             flat = out.cpu().numpy()

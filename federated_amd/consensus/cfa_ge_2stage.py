@@ -123,6 +123,13 @@ class CFA_ge_process:
                         np.asarray(c["grad_weights2"])[..., ii], np.squeeze(np.asarray(c["grad_biases2"]))[..., ii]])
         return out
 
+    # hooks overridden by the mobile-network variant (cfa_ge_2stage_mobilenet.py)
+    def _round_neighbors(self, epoch):
+        return self.get_connectivity(self.ii_saved_local, self.neighbors, self.devices)
+
+    def _states_for_update(self, states, n):
+        return states
+
     def _update(self, W4, states, grads, lr1, lr2, init, use_filtered):
         W = mixer().mewma(W4, states, grads, self.mewma, (lr1, lr1, lr2, lr2), init, use_filtered)
         return _tf1.squeeze_out(*W)
@@ -141,7 +148,7 @@ class CFA_ge_process:
         if epoch == 0:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved
-        nbr_vec = self.get_connectivity(ii, self.neighbors, self.devices)
+        nbr_vec = self._round_neighbors(epoch)
         W = self._stage1_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], nbr_vec, epoch, eps_t_control)
         _tf1.publish(ii, epoch, *W)  # the MIXED model (:203-211)
         wait_for("datamat{}_{}.mat".format(ii, epoch))
@@ -149,10 +156,10 @@ class CFA_ge_process:
         self._publish_gradients(x_train2, y_train2, nbr_vec, epoch, epoch)
         pause(5)
         grads = self._neighbour_gradients(nbr_vec, epoch)
-        states = [W_l1_saved, n_l1_saved, W_l2_saved, n_l2_saved]
+        states = self._states_for_update([W_l1_saved, n_l1_saved, W_l2_saved, n_l2_saved], len(nbr_vec))
         W = self._update(W, states, grads, learning_rate1, learning_rate2, init=(epoch == 1),
                          use_filtered=False)
-        return (*W, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved)
+        return (*W, states[0], states[2], states[1], states[3])
 
     # -- 2-stage (fast) -----------------------------------------------------------------------
     def getFederatedWeight_gradients_fast(self, n_W_l1, n_W_l2, n_b_l1, n_b_l2, epoch, v_loss, eng,
@@ -168,7 +175,7 @@ class CFA_ge_process:
         if epoch == 0:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved
-        nbr_vec = self.get_connectivity(ii, self.neighbors, self.devices)
+        nbr_vec = self._round_neighbors(epoch)
         W = self._stage1_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], nbr_vec, epoch, eps_t_control)
         pause(3)
         _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2)  # PRE-mix model (:470-478)
@@ -181,7 +188,7 @@ class CFA_ge_process:
                     print("Error while deleting file")
         pause(5)
         grads = self._neighbour_gradients(nbr_vec, epoch - 1)
-        states = [W_l1_saved, n_l1_saved, W_l2_saved, n_l2_saved]
+        states = self._states_for_update([W_l1_saved, n_l1_saved, W_l2_saved, n_l2_saved], len(nbr_vec))
         W = self._update(W, states, grads, learning_rate1, learning_rate2, init=False,
                          use_filtered=(self.ML_model == 1))
-        return (*W, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved)
+        return (*W, states[0], states[2], states[1], states[3])

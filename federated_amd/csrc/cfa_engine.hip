@@ -115,6 +115,7 @@ static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
 struct Fanin {
   const float* src[CFA_MAX_FANIN + 1];  // [0] = local (w0), [1..N] = neighbours
   float c[CFA_MAX_FANIN + 1];           // SEQ: c[j] = alpha of src[j] (c[0] unused); LIN: coeff
+  float d[CFA_MAX_FANIN + 1];           // SEQ_DIV: d[j] = divisor of step j (d[0] unused)
 };
 
 template <bool NT>
@@ -139,6 +140,16 @@ __device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
       f4 t = v[j] - w;  // numpy: (x - w)
       t = f.c[j] * t;   //        eps * (...)
       w = w + t;        //        w + (...)
+    }
+    return w;
+  } else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV) {
+    f4 w = v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      f4 t = v[j] - w;  // numpy: (x - w)
+      t = f.c[j] * t;   //        u * (...)
+      t = t / f.d[j];   //        (...) / C   (IEEE-correct fp32 division)
+      w = w + t;
     }
     return w;
   } else {
@@ -255,6 +266,7 @@ struct ScalarFanin {
   const float* src[CFA_MAX_FANIN + 1];
   long long stride[CFA_MAX_FANIN + 1];
   float c[CFA_MAX_FANIN + 1];
+  float d[CFA_MAX_FANIN + 1];
   int n;
 };
 __global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFanin f, long long P,
@@ -265,11 +277,12 @@ __global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFa
        i += (long long)gridDim.x * kBlock) {
     const float w0 = f.src[0][i * f.stride[0]];
     float w;
-    if (rule == CFA_RULE_SEQUENTIAL) {
+    if (rule == CFA_RULE_SEQUENTIAL || rule == CFA_RULE_SEQUENTIAL_DIV) {
       w = w0;
       for (int j = 1; j <= f.n; ++j) {
         float t = f.src[j][i * f.stride[j]] - w;
         t = f.c[j] * t;
+        if (rule == CFA_RULE_SEQUENTIAL_DIV) t = t / f.d[j];
         w = w + t;
       }
     } else {
@@ -514,7 +527,7 @@ static int compress_params(int mode, CompressParams& cp) {
 // a scalar tail. Buckets with different misalignments run entirely on the scalar path.
 static int mix_pass(float* out, const float* local, const float* const* nbrs, const float* c,
                     int n, size_t P, int rule, const CompressParams* cp, hipStream_t st,
-                    const cfa_launch_t& lc = tune()) {
+                    const cfa_launch_t& lc = tune(), const float* div = nullptr) {
   const uintptr_t mis = addr(out) & 15;
   bool same = (addr(local) & 15) == mis;
   for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
@@ -537,6 +550,7 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
     f.src[0] = local + head;
     for (int j = 0; j < n; ++j) f.src[j + 1] = nbrs[j] + head;
     for (int k = 0; k <= n; ++k) f.c[k] = c[k];
+    for (int k = 0; k <= n; ++k) f.d[k] = div ? div[k] : 1.0f;
     if (cp) {
       CompressParams shifted = cpv;
       shifted.cbegin = cpv.cbegin - (long long)head;
@@ -544,6 +558,8 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
       launch_vec_compress(n, st, out + head, f, (long long)nvec, shifted);
     } else if (rule == CFA_RULE_SEQUENTIAL) {
       launch_vec<CFA_RULE_SEQUENTIAL>(n, st, out + head, f, (long long)nvec, lc);
+    } else if (rule == CFA_RULE_SEQUENTIAL_DIV) {
+      launch_vec<CFA_RULE_SEQUENTIAL_DIV>(n, st, out + head, f, (long long)nvec, lc);
     } else {
       launch_vec<CFA_RULE_LINEAR>(n, st, out + head, f, (long long)nvec, lc);
     }
@@ -562,6 +578,7 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
       sf.stride[j + 1] = 1;
     }
     for (int k = 0; k <= n; ++k) sf.c[k] = c[k];
+    for (int k = 0; k <= n; ++k) sf.d[k] = div ? div[k] : 1.0f;
     sf.n = n;
     CompressParams sc = cpv;
     sc.cbegin = cpv.cbegin - (long long)b;
@@ -639,6 +656,33 @@ extern "C" int cfa_mix_seq_ex_f32(float* out, const float* local, const float* c
   if (lc.blocks_per_cu < 0) return fail(CFA_E_INVALID, "blocks_per_cu < 0");
   lc.vec_per_lane = norm_vec(lc.vec_per_lane);
   return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream, lc);
+}
+
+extern "C" int cfa_mix_seq_div_f32(float* out, const float* local, const float* const* nbrs,
+                                   const float* alphas, const float* divisors, int n, size_t P,
+                                   void* stream) {
+  if (n > 0 && (!alphas || !divisors)) return fail(CFA_E_INVALID, "null alphas/divisors");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1], d[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = 1.0f;
+    d[0] = 1.0f;
+    for (int j = 0; j < m; ++j) {
+      c[j + 1] = alphas[done + j];
+      d[j + 1] = divisors[done + j];
+    }
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL_DIV, nullptr, st,
+                          tune(), d))
+      return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
 }
 
 extern "C" int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,

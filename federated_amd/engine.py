@@ -127,6 +127,20 @@ class Engine:
                       self.stream_handle(stream))
         return out
 
+    def mix_seq_div(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                    alphas: Sequence[float], divisors: Sequence[float], stream=None) -> torch.Tensor:
+        """out = fold_j(w <- w + (alphas[j]*(nbrs[j] - w)) / divisors[j]) (FedAvg form)."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P)
+        if not (len(alphas) == len(divisors) == len(nbrs)):
+            raise ValueError("one alpha and one divisor per neighbour required")
+        _lib.call("cfa_mix_seq_div_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(alphas),
+                  _lib.float_array(divisors), len(nbrs), P, self.stream_handle(stream))
+        return out
+
     def mix_linear(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
                    coeff: Sequence[float], stream=None) -> torch.Tensor:
         """out = coeff[0]*local + sum_j coeff[j+1]*nbrs[j]."""

@@ -56,7 +56,9 @@ enum {
    * This reproduces the fp32 numpy chain bit for bit. */
   CFA_RULE_SEQUENTIAL = 0,
   /* Linear combination: out = c_0 * local + sum_j c_{j+1} * x_j (fp32 FMA chain). */
-  CFA_RULE_LINEAR = 1
+  CFA_RULE_LINEAR = 1,
+  /* Sequential rule with a divisor: w <- w + (a_j * (x_j - w)) / d_j (FedAvg form). */
+  CFA_RULE_SEQUENTIAL_DIV = 2
 };
 
 /* Compression epilogue modes (TF1/consensus/cfa_ongraphs.py:225-273). */
@@ -98,6 +100,14 @@ typedef struct {
 CFA_API int cfa_mix_seq_ex_f32(float* out, const float* local, const float* const* nbrs,
                                const float* alphas, int n, size_t P, const cfa_launch_t* launch,
                                void* stream);
+
+/* (f1) FedAvg / parameter-server fold: w <- w + (alphas[j] * (nbrs[j] - w)) / divisors[j],
+ * j = 0..n-1, each step rounded like numpy's `p + u*(x - p)/C` (fp32 multiply, then IEEE fp32
+ * division by the count). Replaces TF2 parameter_server_v2.py:159-161 / parameter_server.py:154,
+ * :74 (metalearning), FL_over_MQTT/PS_server.py:127-134, learner_consensus.py:150-153. */
+CFA_API int cfa_mix_seq_div_f32(float* out, const float* local, const float* const* nbrs,
+                                const float* alphas, const float* divisors, int n, size_t P,
+                                void* stream);
 
 /* Linear-combination mix: out[i] = coeff[0]*local[i] + sum_j coeff[j+1]*nbrs[j][i].
  * The closed form of the sequential rule (c_0 = prod(1-a_j), c_{j+1} = a_j prod_{k>j}(1-a_k)),

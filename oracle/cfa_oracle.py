@@ -221,3 +221,23 @@ def mobile_neighbors(graph: np.ndarray, ii: int, max_neighbors: int, devices: in
     if nb.size > max_neighbors:
         return np.asarray(random.choices(nb, k=max_neighbors))
     return nb
+
+
+# ----------------------------------------------------------------------------------------
+# FedAvg parameter server (f1)
+# ----------------------------------------------------------------------------------------
+
+
+def ps_fedavg(params, models, update_factor, divide: bool = True) -> list:
+    """parameter_server_v2.py:159-161 / parameter_server.py:154, :74:
+    p[q] <- p[q] + u * (x_k[q] - p[q]) / C for k in order (C = number of received models);
+    the transfer-learning branch (:150-157) omits the division (divide=False)."""
+    p = list(params)
+    C = len(models)
+    for q in range(len(p)):
+        for k in range(C):
+            if divide:
+                p[q] = p[q] + update_factor * (models[k][q] - p[q]) / C
+            else:
+                p[q] = p[q] + update_factor * (models[k][q] - p[q])
+    return p

@@ -472,6 +472,110 @@ def case_topology():
     save("topology_kregular.npz", **out)
 
 
+def case_tf1_cfa_ge_mobilenet():
+    ge = load_ref(os.path.join(TF1, "consensus", "cfa_ge_2stage_mobilenet.py"), "ref_tf1_cfa_ge_mn")
+    out = {}
+    K, N, rho, eps, lr1, lr2 = 5, 2, 0.99, 1.0, 0.1, 0.05
+    for variant, epoch in (("fast", 5), ("4stage_e1", 1), ("4stage_e3", 3)):
+        ii = 2
+        tag = f"cnn_{variant}"
+        rng = np.random.default_rng(zlib.crc32(("mn" + tag).encode()))
+        with Workdir():
+            graph = sio.loadmat("consensus/vGraph.mat")["graph"]
+            nbr = [kk for kk in range(K) if graph[ii, kk, epoch] == 1]
+            grad_epoch = epoch - 1 if variant == "fast" else epoch
+            prev = {j: gen_model(rng, SHAPES_CNN_GE) for j in range(K)}
+            grads = {j: [rng.standard_normal(tuple(s) + (K,)) for s in SHAPES_CNN_GE] for j in range(K)}
+            for j in range(K):
+                W1, b1, W2, b2 = prev[j]
+                sio.savemat(f"datamat{j}_{epoch - 1}.mat", {"weights1": W1, "biases1": b1, "weights2": W2, "biases2": b2})
+                if variant != "fast" and j != ii:
+                    sio.savemat(f"datamat{j}_{epoch}.mat", {"weights1": W1, "biases1": b1, "weights2": W2, "biases2": b2})
+                g = grads[j]
+                sio.savemat(f"datagrad{j}_{grad_epoch}.mat", {"grad_weights1": g[0], "grad_biases1": g[1],
+                                                             "grad_weights2": g[2], "grad_biases2": g[3]})
+            local = gen_model(rng, SHAPES_CNN_GE)
+            states = [np.zeros(tuple(s) + (N,)) for s in SHAPES_CNN_GE]
+            p = ge.CFA_ge_process(True, K, ii, N, rho)
+            p.setCNNparameters(16, 8, 5, 5, 21, 8, 512)
+            fn = p.getFederatedWeight_gradients_fast if variant == "fast" else p.getFederatedWeight_gradients
+            W1, b1, W2, b2 = local
+            res = fn(W1, W2, b1, b2, epoch, np.zeros(3), 0, None, None, states[0], states[2], states[1], states[3],
+                     eps, lr1, lr2)
+        out[f"{tag}/meta"] = np.array([K, N, ii, epoch], dtype=np.int64)
+        out[f"{tag}/hyper"] = np.array([rho, eps, lr1, lr2])
+        out[f"{tag}/nbr"] = np.asarray(nbr, dtype=np.int64)
+        for t in range(4):
+            out[f"{tag}/local_{t}"] = local[t]
+            for j in nbr:
+                out[f"{tag}/prev{j}_{t}"] = prev[j][t]
+                out[f"{tag}/grad{j}_{t}"] = grads[j][t][..., ii]
+            out[f"{tag}/out_{t}"] = np.asarray(res[t])
+        for t, r in zip((0, 2, 1, 3), res[4:8]):
+            out[f"{tag}/state_out_{t}"] = np.asarray(r)
+    save("tf1_cfa_ge_mobilenet.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# f1: TF2 FedAvg parameter servers (parameter_server.py, parameter_server_v2.py)
+# --------------------------------------------------------------------------------------
+def case_parameter_server():
+    ps1 = load_ref(os.path.join(TF2, "MNIST_dataset", "consensus", "parameter_server.py"), "ref_ps1")
+    ps1c = load_ref(os.path.join(TF2, "CIFAR100_dataset", "consensus", "parameter_server.py"), "ref_ps1c")
+    ps2 = load_ref(os.path.join(TF2, "MNIST_dataset", "consensus", "parameter_server_v2.py"), "ref_ps2")
+    out = {}
+    D = 7
+    rng = np.random.default_rng(99)
+    models = [gen_model(rng, SHAPES_LENET1) for _ in range(D)]
+    grads = [gen_model(rng, SHAPES_LENET1, 0.1) for _ in range(D)]
+    glob_ = gen_model(rng, SHAPES_LENET1)
+    losses = rng.random(D)
+    indexes_tx = np.stack([rng.permutation(D)[:4] for _ in range(5)], axis=1)  # [active, epochs]
+    for t in range(len(SHAPES_LENET1)):
+        out[f"models_{t}"] = np.stack([m[t] for m in models])
+        out[f"grads_{t}"] = np.stack([g[t] for g in grads])
+        out[f"global_{t}"] = glob_[t]
+    out["losses"] = losses
+    out["indexes_tx"] = indexes_tx
+    cases = [  # (tag, module, method, aggregation_type, active, update_factor, epoch, ended)
+        ("ps1_avg", "ps1", "w", 0, 3, 1, 0, ()),
+        ("ps1_avg_u099", "ps1", "w", 0, 5, 0.99, 0, ()),
+        ("ps1_best", "ps1", "w", 1, 4, 1, 0, ()),
+        ("ps1_meta", "ps1", "meta", 0, 4, 1, 0, ()),
+        ("ps1c_avg", "ps1c", "w", 0, 3, None, 0, ()),
+        ("ps2_avg", "ps2", "w", 0, 4, None, 2, ()),
+        ("ps2_avg_u1", "ps2", "w", 0, 4, 1, 3, ()),
+        ("ps2_end", "ps2", "w", 0, 4, None, 1, (int(indexes_tx[2, 1]),)),
+    ]
+    out["cases"] = np.array([c[0] for c in cases])
+    mods = {"ps1": ps1, "ps1c": ps1c, "ps2": ps2}
+    for tag, modname, method, agg, active, u, epoch, ended in cases:
+        with Workdir():
+            for k in range(D):
+                publish_tf2(k, models[k], 10, k in ended, grads[k])
+                np.savez(f"results/dump_train_variables{k}.npz", epoch_count=10, training_end=k in ended,
+                         loss=losses[k])
+            params = obj_array([a.copy() for a in glob_])
+            kw = {} if u is None else {"update_factor": u}
+            if modname == "ps2":
+                p = mods[modname].Parameter_Server(D, params, active, indexes_tx, **kw)
+            else:
+                p = mods[modname].Parameter_Server(D, params, active, **kw)
+            random.seed(5)
+            if method == "meta":
+                res = p.federated_metalearning(epoch, agg)
+            else:
+                res = p.federated_target_weights_aggregation(epoch, agg)
+            probe = random.random()
+        out[f"{tag}/meta"] = np.array([agg, active, epoch], dtype=np.int64)
+        out[f"{tag}/u"] = np.array(-1.0 if u is None else u)
+        out[f"{tag}/ended"] = np.array(ended, dtype=np.int64)
+        out[f"{tag}/rng_probe"] = np.array(probe)
+        for t in range(len(SHAPES_LENET1)):
+            out[f"{tag}/out_{t}"] = np.asarray(res[t])
+    save("tf2_parameter_server.npz", **out)
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit(f"reference tree not found at {REF}")
@@ -481,7 +585,9 @@ def main():
     case_tf1_cfa()
     case_tf1_ongraphs()
     case_tf1_cfa_ge()
+    case_tf1_cfa_ge_mobilenet()
     case_tf2()
+    case_parameter_server()
 
 
 if __name__ == "__main__":

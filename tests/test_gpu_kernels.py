@@ -203,3 +203,17 @@ def test_error_paths(gpu):
         gpu.mix_seq(x, torch.zeros(8, device="cuda"), [], [])
     with pytest.raises(TypeError):
         gpu.mix_seq(x, torch.zeros(16, device="cuda", dtype=torch.float64), [], [])
+
+
+@pytest.mark.parametrize("n", [1, 3, 7, 20])
+def test_mix_seq_div_bitexact(gpu, n):
+    """FedAvg form p <- p + u*(x - p)/C (parameter_server_v2.py:159-161), fp32 numpy rounding."""
+    rng = np.random.default_rng(600 + n)
+    P = 1_000_003
+    p = _rand(rng, 1, P)[0]
+    xs = _rand(rng, n, P)
+    for u in (1, 0.99):
+        ref = O.ps_fedavg([p], [[x] for x in xs], u)[0]
+        out = torch.empty(P, dtype=torch.float32, device="cuda")
+        gpu.mix_seq_div(out, _dev(p), [_dev(x) for x in xs], [u] * n, [float(n)] * n)
+        assert np.array_equal(out.cpu().numpy(), ref), (n, u)

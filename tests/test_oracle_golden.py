@@ -152,3 +152,25 @@ def test_closed_form_equals_sequential_in_exact_arithmetic():
         seq = seq + a * (x - seq)
     assert c[0] * w + sum(cj * x for cj, x in zip(c[1:], xs)) == seq
     assert sum(c) == 1
+
+
+@pytest.mark.parametrize("variant", ["fast", "4stage_e1", "4stage_e3"])
+def test_tf1_cfa_ge_mobilenet_oracle(variant):
+    """cfa_ge_2stage_mobilenet.py: vGraph neighbours of the epoch, states re-zeroed per call."""
+    z = load_golden("tf1_cfa_ge_mobilenet.npz")
+    tag = f"cnn_{variant}"
+    K, N, ii, epoch = (int(x) for x in z[f"{tag}/meta"])
+    rho, eps, lr1, lr2 = (float(x) for x in z[f"{tag}/hyper"])
+    nbr = z[f"{tag}/nbr"].tolist()
+    graph = load_golden("topology_mobile.npz")["graph"]
+    assert nbr == [kk for kk in range(K) if graph[ii, kk, epoch] == 1]
+    local = [z[f"{tag}/local_{t}"] for t in range(4)]
+    prev = [[z[f"{tag}/prev{j}_{t}"] for t in range(4)] for j in nbr]
+    W = O.tf1_mix(local, prev, eps, [O.tf1_weight_factor(K, ii, j, N - 1) for j in nbr])
+    states = [np.zeros(z[f"{tag}/state_out_{t}"].shape) for t in range(4)]
+    grads = [[z[f"{tag}/grad{j}_{t}"] for t in range(4)] for j in nbr]
+    W = O.tf1_mewma(W, states, grads, rho, lr1, lr2, use_filtered=(variant == "fast"), init=(variant == "4stage_e1"))
+    for t in range(4):
+        ref = z[f"{tag}/out_{t}"]
+        assert np.array_equal(np.asarray(W[t]).reshape(ref.shape), ref), (variant, t)
+        assert np.array_equal(states[t], z[f"{tag}/state_out_{t}"]), (variant, "state", t)
