@@ -39,7 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--params", type=int, default=25_000_000, help="P, fp32 params per bucket")
     p.add_argument("--neighbours", type=int, default=8, help="K (even: ring window K/2 per side)")
-    p.add_argument("--devices-per-gpu", type=int, default=64)
+    p.add_argument("--devices-per-gpu", type=int, default=128,
+                   help="simulated devices per GPU (128 x 100 MB models + outputs = 26 GB of HBM)")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
