@@ -6,15 +6,17 @@ its neighbours' models every round (TF1 ``FL_CFA_CNN_tf2.py:317-319``, TF2
 device-resident: shard ``r`` of ``world`` owns devices ``[r*L, (r+1)*L)`` as one stacked
 ``[L, P]`` fp32 tensor in HBM (288 GB per MI355X holds thousands of 25M-parameter models).
 
-Topology: a ring window of ``h`` in-neighbours on each side (K = 2h neighbours), the
-wrap-around form of the k-regular window ``get_connectivity`` (TF1 ``cfa.py:14-32``) that
-TF2 ``consensus_v4.py:133-137`` uses for its ring. Neighbour order is ascending device offset
-(g-h, ..., g-1, g+1, ..., g+h), the order the reference's window lists them. The mixing rule is
-the TF2 policy eps = 1/(K+1) applied sequentially (``consensus_v3.py:145,153-155``).
+Topology: a wrap-around ring window of ``h_left`` neighbours below and ``h_right`` above each
+device (K = h_left + h_right): the symmetric form (h, h) is the wrap-around k-regular window
+of ``get_connectivity`` (TF1 ``cfa.py:14-32``); (1, 0) is the TF2 v4 / FL_radar ring rule for
+N < 2 (in-neighbour ii-1, ``consensus_v4.py:133-137``). Neighbour order is ascending device
+offset (g-h_left, ..., g-1, g+1, ..., g+h_right), the order the reference's window lists them.
+The mixing rule is the TF2 policy eps = 1/(K+1) applied sequentially (``consensus_v3.py:145,
+153-155``).
 
-A round = (1) halo exchange: the h first / h last buckets of each shard go to the previous /
-next shard (one message per side, RCCL over xGMI), overlapped with (2) the mixes of the
-interior devices, which need no remote bucket, then (3) the mixes of the 2h boundary devices.
+A round = (1) halo exchange: the h_right first / h_left last buckets of each shard go to the
+previous / next shard (one RCCL message per bucket, over xGMI), overlapped with (2) the mixes of
+the interior devices, which need no remote bucket, then (3) the mixes of the boundary devices.
 """
 from __future__ import annotations
 
@@ -26,15 +28,19 @@ import torch
 class RingShardPlan:
     """Index bookkeeping for one shard (pure host logic; testable on CPU)."""
 
-    def __init__(self, rank: int, world: int, devices_per_shard: int, half_window: int):
-        if devices_per_shard < 1 or half_window < 0:
-            raise ValueError("need >= 1 device per shard and a non-negative window")
-        if world > 1 and devices_per_shard < half_window:
-            raise ValueError("a shard must hold at least `half_window` devices")
-        if 2 * half_window >= devices_per_shard * world:
+    def __init__(self, rank: int, world: int, devices_per_shard: int, half_window: int,
+                 right_window: Optional[int] = None):
+        hl = half_window
+        hr = half_window if right_window is None else right_window
+        if devices_per_shard < 1 or hl < 0 or hr < 0:
+            raise ValueError("need >= 1 device per shard and non-negative windows")
+        if world > 1 and devices_per_shard < max(hl, hr):
+            raise ValueError("a shard must hold at least as many devices as each window side")
+        if hl + hr >= devices_per_shard * world:
             raise ValueError("ring window wider than the population")
         self.rank, self.world = rank, world
-        self.L, self.h = devices_per_shard, half_window
+        self.L, self.hl, self.hr = devices_per_shard, hl, hr
+        self.h = max(hl, hr)
         self.D = devices_per_shard * world
         self.first = rank * devices_per_shard
         self.left = (rank - 1) % world
@@ -42,12 +48,12 @@ class RingShardPlan:
 
     @property
     def K(self) -> int:
-        return 2 * self.h
+        return self.hl + self.hr
 
     def neighbours(self, g: int) -> List[int]:
         """Global neighbour ids of global device g, in mixing order."""
-        h, D = self.h, self.D
-        return [(g + o) % D for o in list(range(-h, 0)) + list(range(1, h + 1))]
+        D = self.D
+        return [(g + o) % D for o in list(range(-self.hl, 0)) + list(range(1, self.hr + 1))]
 
     def locate(self, g: int) -> Tuple[str, int]:
         """Where global device g's bucket lives on this shard: ('local', row), ('left', row) or
@@ -57,9 +63,9 @@ class RingShardPlan:
             return "local", rel
         if self.world == 1:
             raise KeyError(g)
-        if rel >= self.D - self.h:  # just below our first device: left halo
-            return "left", rel - (self.D - self.h)
-        if rel < self.L + self.h:   # just above our last device: right halo
+        if self.hl and rel >= self.D - self.hl:  # just below our first device: left halo
+            return "left", rel - (self.D - self.hl)
+        if self.hr and rel < self.L + self.hr:   # just above our last device: right halo
             return "right", rel - self.L
         raise KeyError(f"device {g} is not reachable from shard {self.rank}")
 
@@ -67,7 +73,7 @@ class RingShardPlan:
         """Does local device i (0-based in the shard) read a remote bucket?"""
         if self.world == 1:
             return False
-        return i < self.h or i >= self.L - self.h
+        return i < self.hl or i >= self.L - self.hr
 
     def interior(self) -> List[int]:
         return [i for i in range(self.L) if not self.needs_halo(i)]
@@ -76,14 +82,17 @@ class RingShardPlan:
         return [i for i in range(self.L) if self.needs_halo(i)]
 
     def halo_transfers(self):
-        """(sends, recvs) as (row slice of the local stack or halo name, peer). Order is chosen
-        so that with world == 2 (left == right peer) the k-th send to a peer matches that peer's
-        k-th receive: first the message that becomes the right neighbour's LEFT halo, then the one
-        that becomes the left neighbour's RIGHT halo; receives left halo first, then right."""
-        if self.world == 1 or self.h == 0:
+        """(sends, recvs): sends = [(local row, peer)], recvs = [((halo name, row), peer)], one
+        bucket per message. The order makes the k-th send to a peer match that peer's k-th
+        receive even when world == 2 (left == right peer): first the buckets that become the
+        right neighbour's LEFT halo (our last hl rows, ascending), then those that become the
+        left neighbour's RIGHT halo (our first hr rows); receives left halo rows, then right."""
+        if self.world == 1:
             return [], []
-        sends = [(slice(self.L - self.h, self.L), self.right), (slice(0, self.h), self.left)]
-        recvs = [("left", self.left), ("right", self.right)]
+        sends = [(r, self.right) for r in range(self.L - self.hl, self.L)]
+        sends += [(r, self.left) for r in range(self.hr)]
+        recvs = [(("left", r), self.left) for r in range(self.hl)]
+        recvs += [(("right", r), self.right) for r in range(self.hr)]
         return sends, recvs
 
 
@@ -94,12 +103,11 @@ class RingPopulationShard:
                  dtype=torch.float32):
         self.plan, self.P = plan, int(P)
         self.device = torch.device(device)
-        h = plan.h
         self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
         self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
         self.halo = {
-            "left": torch.empty((h, self.P), dtype=dtype, device=self.device),
-            "right": torch.empty((h, self.P), dtype=dtype, device=self.device),
+            "left": torch.empty((plan.hl, self.P), dtype=dtype, device=self.device),
+            "right": torch.empty((plan.hr, self.P), dtype=dtype, device=self.device),
         }
         self.transport = transport
         self.engine = engine
@@ -117,8 +125,8 @@ class RingPopulationShard:
         sends, recvs = self.plan.halo_transfers()
         if not sends and not recvs:
             return
-        s = [(self.models[sl].reshape(-1), peer) for sl, peer in sends]
-        r = [(self.halo[name].reshape(-1), peer) for name, peer in recvs]
+        s = [(self.models[row], peer) for row, peer in sends]
+        r = [(self.halo[name][row], peer) for (name, row), peer in recvs]
         self.transport.exchange(s, r, stream)
 
     def mix_device(self, i: int, stream=None) -> None:

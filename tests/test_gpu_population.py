@@ -67,3 +67,60 @@ def test_host_staging_e2e_small(gpu):
     r = measure_e2e(gpu, 1_000_003, 4, reps=2, chunks=4)
     assert r["pipelined_equals_device_result"]
     assert r["serial"]["ms"] > 0 and r["h2d_GBps"] > 0
+
+
+def _pop_tables(L, plan_or_lists, alphas_fn, buckets, outs):
+    ptr, idx, coef = [0], [], []
+    for i in range(L):
+        nbr = plan_or_lists(i)
+        idx += [i] + list(nbr)
+        coef += [1.0] + alphas_fn(len(nbr))
+        ptr.append(len(idx))
+    t64 = lambda xs: torch.tensor([x.data_ptr() for x in xs], dtype=torch.int64, device="cuda")
+    return (t64(outs), t64(buckets), torch.tensor(ptr, dtype=torch.int32, device="cuda"),
+            torch.tensor(idx, dtype=torch.int32, device="cuda"),
+            torch.tensor(coef, dtype=torch.float32, device="cuda"))
+
+
+@pytest.mark.parametrize("name,D,P,nbr_fn,alpha_fn", [
+    # config 2: FL_CFA_CNN_tf2 shapes (P = 24 622), 8 devices, K = 3 (cfa_ongraphs alpha = eps/(1+n))
+    ("cfg2_cnn_8dev_K3", 8, 24_622, lambda i, D: [(i + o) % D for o in (-1, 1, 2)], lambda n: [1.0 / (1 + n)] * n),
+    # config 3 topology: CFA-GE CNN (P = 1 488), 16 devices, k-regular N = 2 (cfa.py alpha 1/N)
+    ("cfg3_cnn_ge_16dev", 16, 1_488, None, lambda n: [0.5] * n),
+    # config 4: CIFAR-100 VGG-1 (P = 1 071 748), 32 devices, K = 4 ring window, eps = 1/(K+1)
+    ("cfg4_vgg1_32dev_K4", 32, 1_071_748, lambda i, D: [(i + o) % D for o in (-2, -1, 1, 2)], lambda n: [1.0 / (n + 1)] * n),
+    # config 5: radar (P = 24 622), 128 devices, ring in-neighbour ii-1 (consensus_v4 N < 2), eps = 1/2
+    ("cfg5_radar_128dev_ring", 128, 24_622, lambda i, D: [(i - 1) % D], lambda n: [1.0 / (n + 1)] * n),
+])
+def test_config_shapes_population_kernel(gpu, name, D, P, nbr_fn, alpha_fn):
+    """The functional BASELINE configs as one-launch population rounds (cfa_mix_population_f32),
+    bit-exact against per-device sequential mixes on the oracle."""
+    from oracle.cfa_oracle import tf1_kregular
+    if nbr_fn is None:
+        nbr_fn = lambda i, D: tf1_kregular(i, 2, D).tolist()
+    g = torch.Generator(device="cuda").manual_seed(D * 7 + P)
+    buckets = [torch.randn(P, generator=g, device="cuda") for _ in range(D)]
+    outs = [torch.empty(P, device="cuda") for _ in range(D)]
+    tables = _pop_tables(D, lambda i: nbr_fn(i, D), alpha_fn, buckets, outs)
+    gpu.population(*tables, D, 0, P)
+    torch.cuda.synchronize()
+    host = [b.cpu().numpy() for b in buckets]
+    for i in range(D):
+        nbr = nbr_fn(i, D)
+        ref = sequential_mix(host[i], [host[j] for j in nbr], alpha_fn(len(nbr)))
+        assert np.array_equal(outs[i].cpu().numpy(), ref), (name, i)
+
+
+def test_config5_ring_round_world1(gpu):
+    """Config 5 topology through the shard round (one-sided ring window)."""
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    plan = RingShardPlan(0, 1, 128, 1, 0)
+    shard = RingPopulationShard(plan, 24_622, torch.device("cuda"), None, gpu)
+    shard.models.normal_()
+    shard.round()
+    torch.cuda.synchronize()
+    h = shard.models.cpu().numpy()
+    out = shard.mixed.cpu().numpy()
+    assert shard.alphas == [0.5]
+    for i in (0, 1, 77, 127):
+        assert np.array_equal(out[i], sequential_mix(h[i], [h[(i - 1) % 128]], [0.5]))

@@ -60,31 +60,32 @@ def test_bucket_layout_roundtrip():
         lay.pack(arrays[:3])
 
 
-@pytest.mark.parametrize("world,L,h", [(1, 8, 2), (2, 8, 4), (4, 6, 3), (8, 64, 4), (3, 5, 2)])
-def test_ring_shard_plan(world, L, h):
+@pytest.mark.parametrize("world,L,hl,hr", [(1, 8, 2, 2), (2, 8, 4, 4), (4, 6, 3, 3), (8, 64, 4, 4),
+                                           (3, 5, 2, 2), (8, 16, 1, 0), (4, 8, 2, 1)])
+def test_ring_shard_plan(world, L, hl, hr):
     from federated_amd.population import RingShardPlan
     D = world * L
     for r in range(world):
-        p = RingShardPlan(r, world, L, h)
+        p = RingShardPlan(r, world, L, hl, hr)
         for i in range(L):
             g = p.first + i
             nb = p.neighbours(g)
-            assert len(nb) == 2 * h and g not in nb and len(set(nb)) == 2 * h
-            assert nb == sorted(nb, key=lambda j: ((j - g + D // 2) % D))  # ascending offsets
+            assert len(nb) == hl + hr and g not in nb and len(set(nb)) == hl + hr
+            assert nb == [(g + o) % D for o in list(range(-hl, 0)) + list(range(1, hr + 1))]
             for j in nb:
                 where, row = p.locate(j)
                 if where == "local":
                     assert p.first + row == j
                 elif where == "left":
-                    assert (p.first - h + row) % D == j
+                    assert (p.first - hl + row) % D == j
                 else:
                     assert (p.first + L + row) % D == j
             remote = any(p.locate(j)[0] != "local" for j in nb)
-            assert remote == p.needs_halo(i) or (not remote and p.needs_halo(i))
+            assert remote or not p.needs_halo(i) or world == 1
         assert sorted(p.interior() + p.boundary()) == list(range(L))
 
 
-def _gloo_worker(rank, world, port, L, h, P, q):
+def _gloo_worker(rank, world, port, L, h, P, q, hr=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -92,7 +93,7 @@ def _gloo_worker(rank, world, port, L, h, P, q):
         from federated_amd.dist import TorchTransport
         from federated_amd.population import RingPopulationShard, RingShardPlan
         from oracle.cfa_oracle import sequential_mix
-        plan = RingShardPlan(rank, world, L, h)
+        plan = RingShardPlan(rank, world, L, h, hr)
         shard = RingPopulationShard(plan, P, "cpu", TorchTransport())
         for i in range(L):
             g = torch.Generator().manual_seed(1000 + plan.first + i)
@@ -113,15 +114,17 @@ def _gloo_worker(rank, world, port, L, h, P, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,L,h", [(2, 8, 4), (2, 5, 2), (3, 4, 2)])
-def test_sharded_population_exchange_gloo(world, L, h):
+@pytest.mark.parametrize("world,L,h,hr", [(2, 8, 4, 4), (2, 5, 2, 2), (3, 4, 2, 2),
+                                          (8, 16, 1, 0),   # config 5: ring (v4 N=1), 128 devices / 8
+                                          (4, 8, 2, 2)])   # config 4: 32 devices, K=4, 4 shards
+def test_sharded_population_exchange_gloo(world, L, h, hr):
     """Multi-process (gloo) check of the N > 1 path: halo exchange places every remote
     neighbour bucket where the mix reads it, and each shard's mixes equal the unsharded
     population's (oracle on both sides)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + (os.getpid() % 1000) + world * 7 + L
-    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, L, h, 1000, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, L, h, 1000, q, hr)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
