@@ -1,0 +1,116 @@
+"""Topology service: the reference's neighbour-selection rules emitted as CSR
+tables for the one-launch population kernel (``cfa_mix_population_f32``).
+
+The reference computes each device's neighbour list inside that device's process
+(TF1 ``cfa.py:14-32``, ``cfa_ongraphs.py:18-52``; TF2 ``consensus_v3.py:44-70``,
+``consensus_v4.py:111-173``) and its mixing coefficients from an eps policy. For a simulated
+population resident on one GPU, this module builds, for all D devices at once:
+
+    csr_ptr[D+1], csr_idx[E], csr_coef[E]  (first entry of each row = the device itself)
+
+with the same ordered neighbour lists (the same random draws when the rule is random, using
+the same RNG calls) and the same per-step alphas, so one launch reproduces D per-device calls.
+"""
+from __future__ import annotations
+
+import random
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .consensus import _tf1, _tf2
+from .engine import Engine
+
+RULE_SEQUENTIAL = 0
+
+
+# -- neighbour lists for every device ---------------------------------------------------------
+def kregular_tf1(devices: int, neighbors: int) -> List[List[int]]:
+    """cfa.py:14-32 for every device."""
+    return [_tf1.kregular(ii, neighbors, devices).tolist() for ii in range(devices)]
+
+
+def kregular_v3(devices: int, neighbors: int) -> List[List[int]]:
+    """consensus_v3.py:44-70 for every device (at least 2 neighbours)."""
+    return [_tf2.kregular_v3(ii, neighbors, devices).tolist() for ii in range(devices)]
+
+
+def ring_v4(devices: int, neighbors: int) -> List[List[int]]:
+    """consensus_v4.py:111-141 for every device (N < 2: in-neighbour ii-1)."""
+    return [np.atleast_1d(_tf2.kregular_ring(ii, neighbors, devices)).tolist() for ii in range(devices)]
+
+
+def mobile(graph: np.ndarray, g: int, max_neighbors: Optional[int] = None, devices: Optional[int] = None,
+           rng: Optional[random.Random] = None) -> List[List[int]]:
+    """Row ii of adjacency ``graph[:, :, g]`` for every device (cfa_mobilenet.py:36-47); with
+    ``max_neighbors`` the cfa_ongraphs.py:46-48 draw ``random.choices(k=max_neighbors)`` (with
+    replacement) is applied per device in device order, on ``rng`` (default: the global
+    ``random`` module, as the reference)."""
+    devices = graph.shape[0] if devices is None else devices
+    draw = (rng or random).choices
+    out = []
+    for ii in range(devices):
+        row = graph[ii, :, g]
+        nb = [kk for kk in range(devices) if row[kk] == 1]
+        if max_neighbors is not None and len(nb) > max_neighbors:
+            nb = [int(x) for x in draw(np.asarray(nb, dtype=np.uint8), k=max_neighbors)]
+        out.append(nb)
+    return out
+
+
+# -- eps policies: per-step alphas of the sequential rule -------------------------------------
+def alphas_tf2(nbrs: Sequence[int], ii: int, devices: int) -> List[float]:
+    """TF2 weights (consensus_v3.py:145): eps = 1/(n+1) for every step."""
+    n = len(nbrs)
+    return [1 / (n + 1)] * n
+
+
+def alphas_tf1_cfa(eps: float, neighbors: int) -> Callable:
+    """cfa.py:66-69: eps * b/(b + (N-1) b) with N the configured neighbour count."""
+    return lambda nbrs, ii, devices: [eps * _tf1.weight_factor(devices, ii, int(j), neighbors - 1) for j in nbrs]
+
+
+def alphas_tf1_ongraphs(eps: float) -> Callable:
+    """cfa_ongraphs.py:109-113: eps * b/(b + n b) with n this call's neighbour count."""
+    return lambda nbrs, ii, devices: [eps * _tf1.weight_factor(devices, ii, int(j), len(nbrs)) for j in nbrs]
+
+
+def csr(lists: Sequence[Sequence[int]], policy: Callable, devices: Optional[int] = None):
+    """(ptr, idx, coef) numpy arrays; row d = [d] + lists[d], coef = [1] + alphas."""
+    D = len(lists) if devices is None else devices
+    ptr, idx, coef = [0], [], []
+    for d, nb in enumerate(lists):
+        idx += [d] + [int(j) for j in nb]
+        coef += [1.0] + [float(a) for a in policy(nb, d, D)]
+        ptr.append(len(idx))
+    return (np.asarray(ptr, dtype=np.int32), np.asarray(idx, dtype=np.int32),
+            np.asarray(coef, dtype=np.float32))
+
+
+class PopulationRound:
+    """A population of D device buckets resident in HBM, mixed in ONE launch per round."""
+
+    def __init__(self, engine: Engine, models: torch.Tensor, out: Optional[torch.Tensor] = None):
+        if models.dim() != 2 or models.dtype != torch.float32 or not models.is_cuda:
+            raise ValueError("models must be a [D, P] fp32 CUDA tensor")
+        self.engine = engine
+        self.models = models
+        self.out = torch.empty_like(models) if out is None else out
+        D = models.shape[0]
+        dev = models.device
+        self.src = torch.tensor([models[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
+        self.dst = torch.tensor([self.out[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
+        self.tables = None
+
+    def set_topology(self, lists, policy) -> None:
+        ptr, idx, coef = csr(lists, policy, self.models.shape[0])
+        dev = self.models.device
+        self.tables = tuple(torch.from_numpy(a).to(dev) for a in (ptr, idx, coef))
+
+    def run(self, stream=None) -> torch.Tensor:
+        if self.tables is None:
+            raise RuntimeError("set_topology() first")
+        D, P = self.models.shape
+        self.engine.population(self.dst, self.src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
+        return self.out

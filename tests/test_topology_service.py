@@ -1,0 +1,75 @@
+"""Topology service (f4): CSR tables built from the reference's rules (pinned by the golden
+neighbour lists), and one-launch population rounds against per-device oracle mixes (GPU)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, ragged
+from oracle import cfa_oracle as O
+
+
+def test_lists_match_reference_golden():
+    from federated_amd import topology as T
+    z = load_golden("topology_kregular.npz")
+    for name, fn in (("tf1", T.kregular_tf1), ("v3", T.kregular_v3), ("v4", T.ring_v4)):
+        table = ragged(z[f"{name}_keys"], z[f"{name}_len"], z[f"{name}_vals"])
+        for K in (5, 8, 16, 32, 128):
+            for N in (1, 2, 3, 4):
+                lists = fn(K, N)
+                assert [table[(K, N, ii)] for ii in range(K)] == lists, (name, K, N)
+
+
+def test_mobile_lists_match_reference_random_draws():
+    from federated_amd import topology as T
+    z = load_golden("topology_mobile.npz")
+    table = ragged(z["mn_keys"], z["mn_len"], z["mn_vals"])
+    graph = z["graph"]
+    for g in range(0, graph.shape[2], 7):
+        for mx in (1, 2, 3, 4):
+            for ii in range(5):  # golden draws were seeded per (g, ii, mx)
+                random.seed(g * 1000 + ii * 10 + mx)
+                nb = O.mobile_neighbors(graph, ii, mx, 5, g).tolist()
+                assert nb == table[(g, ii, mx, g * 1000 + ii * 10 + mx)]
+        random.seed(123)
+        lists = T.mobile(graph, g, 2)
+        random.seed(123)
+        assert lists == [O.mobile_neighbors(graph, ii, 2, 5, g).tolist() for ii in range(5)]
+
+
+def test_csr_tables_policies():
+    from federated_amd import topology as T
+    lists = T.kregular_tf1(8, 3)
+    ptr, idx, coef = T.csr(lists, T.alphas_tf1_cfa(0.7, 3))
+    assert ptr[0] == 0 and ptr[-1] == len(idx) == len(coef) == 8 + sum(len(l) for l in lists)
+    for d in range(8):
+        row = idx[ptr[d]:ptr[d + 1]].tolist()
+        assert row == [d] + lists[d]
+        a = coef[ptr[d] + 1:ptr[d + 1]]
+        assert np.allclose(a, [0.7 * float(O.tf1_weight_factor(8, d, j, 2)) for j in lists[d]])
+    _, _, c2 = T.csr([[1, 2]], T.alphas_tf2)
+    assert c2.tolist() == [1.0, np.float32(1 / 3), np.float32(1 / 3)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", ["tf1_cfa", "tf1_ongraphs", "tf2"])
+def test_population_round_matches_per_device_calls(gpu, rule):
+    from federated_amd import topology as T
+    D, P = 16, 200_003
+    models = torch.randn(D, P, device="cuda")
+    pr = T.PopulationRound(gpu, models)
+    if rule == "tf1_cfa":
+        lists, pol = T.kregular_tf1(D, 3), T.alphas_tf1_cfa(1.0, 3)
+    elif rule == "tf1_ongraphs":
+        lists, pol = T.kregular_tf1(D, 2), T.alphas_tf1_ongraphs(0.8)
+    else:
+        lists, pol = T.ring_v4(D, 1), T.alphas_tf2
+    pr.set_topology(lists, pol)
+    out = pr.run()
+    torch.cuda.synchronize()
+    host = models.cpu().numpy()
+    for d in range(D):
+        a = [float(np.float32(x)) for x in pol(lists[d], d, D)]
+        ref = O.sequential_mix(host[d], [host[j] for j in lists[d]], a)
+        assert np.array_equal(out[d].cpu().numpy(), ref), (rule, d)
