@@ -211,10 +211,21 @@ __device__ __forceinline__ void block_add_count(unsigned kept, unsigned long lon
 // Vector mix kernel: tiles of kBlock*U float4 per block, grid-stride over tiles; the last
 // partial tile is handled with per-vector guards by the block that owns it.
 // ------------------------------------------------------------------------------------------
+// Streaming-policy store (NT kernels): write-through with sc1, so the once-written output does
+// not leave dirty lines in the XCD's L2 (measured +3% over an nt store on this kernel,
+// tools/tune_cache_policy.py). Buffer stores take 32-bit offsets: the host splits the vector
+// body into launches of at most kMaxChunkVec float4 (2 GiB).
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+constexpr long long kMaxChunkVec = 1LL << 27;
+constexpr int kStoreSc1 = 16;
+
 template <int N, int RULE, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, long long nvec) {
   constexpr long long kTile = (long long)kBlock * U;
   const long long full = nvec / kTile;
+  // (unused and removed by the compiler when !NT)
+  const __amdgpu_buffer_rsrc_t w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
   for (long long t = blockIdx.x; t < full; t += gridDim.x) {
     const long long base = t * kTile + threadIdx.x;
     f4 v[U][N + 1];
@@ -223,7 +234,14 @@ __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, lo
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u][k] = ld4<NT>(f.src[k], base + (long long)u * kBlock);
 #pragma unroll
-    for (int u = 0; u < U; ++u) st4<NT>(out, base + (long long)u * kBlock, fold<N, RULE>(v[u], f));
+    for (int u = 0; u < U; ++u) {
+      const f4 y = fold<N, RULE>(v[u], f);
+      if constexpr (NT)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      else
+        st4<false>(out, base + (long long)u * kBlock, y);
+    }
   }
   if (blockIdx.x == (unsigned)(full % gridDim.x)) {
     for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
@@ -474,8 +492,24 @@ static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const
 }
 
 template <int RULE>
+static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                             const cfa_launch_t& t);
+
+template <int RULE>
 static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
                        const cfa_launch_t& t) {
+  // chunks of at most kMaxChunkVec float4 (32-bit buffer offsets of the streaming store)
+  for (long long done = 0; done < nvec; done += kMaxChunkVec) {
+    const long long m = (nvec - done) < kMaxChunkVec ? (nvec - done) : kMaxChunkVec;
+    Fanin g = f;
+    for (int k = 0; k <= n; ++k) g.src[k] = f.src[k] + done * 4;
+    launch_vec_chunk<RULE>(n, st, out + done * 4, g, m, t);
+  }
+}
+
+template <int RULE>
+static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                             const cfa_launch_t& t) {
   const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : auto_vec(n);
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   const unsigned grid = grid_for(tiles, t);
@@ -872,4 +906,90 @@ extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const
     if (int rc = check_launch("population_tail")) return rc;
   }
   return CFA_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Experiment (not part of the public header): the N = 8, 4-vector mix through buffer loads /
+// stores with explicit gfx950 cache-policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1), used by
+// tools/tune_cache_policy.py to pick the streaming policy of the production kernel.
+// ------------------------------------------------------------------------------------------
+namespace {
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+template <int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void mix8_buf_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  const unsigned bytes = (unsigned)(nvec * 16);
+  __amdgpu_buffer_rsrc_t r[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc((void*)f.src[k], 0, bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, bytes, 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const int base = (int)((t * kTile + threadIdx.x) * 16);
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u4 x = __builtin_amdgcn_raw_buffer_load_b128(r[k], base + u * kBlock * 16, 0, LAUX);
+        v[u][k] = __builtin_bit_cast(f4, x);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w, base + u * kBlock * 16, 0, SAUX);
+    }
+  }
+}
+// global nt loads (as the production kernel) + buffer store with explicit policy
+template <int SAUX>
+__global__ __launch_bounds__(kBlock) void mix8_gld_bst_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                             (int)((base + (long long)u * kBlock) * 16), 0, SAUX);
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int laux, int saux, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_X(L, S) \
+  if (laux == L && saux == S) { mix8_buf_kernel<L, S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_buf"); }
+  CFA_X(0, 0) CFA_X(2, 2) CFA_X(2, 0) CFA_X(0, 2) CFA_X(1, 2) CFA_X(16, 2) CFA_X(17, 2) CFA_X(3, 2)
+  CFA_X(18, 2) CFA_X(19, 2) CFA_X(2, 16) CFA_X(2, 17) CFA_X(2, 18) CFA_X(2, 19) CFA_X(18, 18) CFA_X(17, 17)
+  CFA_X(16, 16) CFA_X(1, 1)
+#undef CFA_X
+#define CFA_G(S) \
+  if (laux == -2 && saux == S) { mix8_gld_bst_kernel<S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_gld"); }
+  CFA_G(0) CFA_G(2) CFA_G(16) CFA_G(17) CFA_G(18) CFA_G(1)
+#undef CFA_G
+  return fail(CFA_E_INVALID, "policy pair not instantiated");
 }

@@ -217,3 +217,21 @@ def test_mix_seq_div_bitexact(gpu, n):
         out = torch.empty(P, dtype=torch.float32, device="cuda")
         gpu.mix_seq_div(out, _dev(p), [_dev(x) for x in xs], [u] * n, [float(n)] * n)
         assert np.array_equal(out.cpu().numpy(), ref), (n, u)
+
+
+def test_mix_seq_bucket_larger_than_2gib(gpu):
+    """Buckets beyond the 32-bit buffer-offset range of the streaming store are split into
+    <= 2 GiB launches; check windows at the start, around the chunk seam and at the end."""
+    P = (1 << 29) + 12_345  # 2.15 GB per fp32 bucket
+    g = torch.Generator(device="cuda").manual_seed(5)
+    local = torch.randn(P, generator=g, device="cuda")
+    nb = torch.randn(P, generator=g, device="cuda")
+    out = torch.empty_like(local)
+    gpu.mix_seq(out, local, [nb], [0.5])
+    seam = 4 * (1 << 27)
+    for a in (0, seam - 4096, P - 8192):
+        sl = slice(a, a + 8192)
+        ref = O.sequential_mix(local[sl].cpu().numpy(), [nb[sl].cpu().numpy()], [0.5])
+        assert np.array_equal(out[sl].cpu().numpy(), ref), a
+    del local, nb, out
+    torch.cuda.empty_cache()
