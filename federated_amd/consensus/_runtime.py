@@ -86,6 +86,20 @@ class HostMixer:
         host = torch.from_numpy(layout.pack(arrays))
         return host.to(self.engine.device, non_blocking=False)
 
+    def _cached(self, kind: str, n: int, dtype=torch.float32, pinned: bool = False) -> torch.Tensor:
+        """Per-thread cached staging buffer (pinned host or device) of at least n elements."""
+        cache = getattr(self._tls, "bufs", None)
+        if cache is None:
+            cache = self._tls.bufs = {}
+        t = cache.get((kind, dtype))
+        if t is None or t.numel() < n:
+            if pinned:
+                t = torch.empty(max(n, 1), dtype=dtype, pin_memory=True)
+            else:
+                t = torch.empty(max(n, 1), dtype=dtype, device=self.engine.device)
+            cache[(kind, dtype)] = t
+        return t[:n]
+
     def mix(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float],
             compress: Optional[Tuple[int, int]] = None,
             divisors: Optional[Sequence[float]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
@@ -94,26 +108,43 @@ class HostMixer:
         ``compress=(mode, layer)`` fuses the cfa_ongraphs compression epilogue on that layer
         (with the pre-mix local as DPCM reference) and returns the kept count.
         ``divisors`` selects the FedAvg form w <- w + (alphas[j] * (x_j - w)) / divisors[j].
+
+        Host path: the local and all neighbour buckets are packed into ONE cached
+        pinned staging buffer and moved by one async H2D copy; the result (and the kept count)
+        come back by async D2H into pinned memory; one stream synchronisation per call.
         Returns (fp32 arrays with the local shapes, kept count or None)."""
         layout = BucketLayout.of(local)
-        with torch.cuda.stream(self._stream()):
-            d_local = self._upload(layout, local)
-            d_nbrs = [self._upload(layout, x) for x in nbrs]
-            out = torch.empty_like(d_local)
+        P, n = layout.P, len(nbrs)
+        st = self._stream()
+        with torch.cuda.stream(st):
+            host = self._cached("h_in", (n + 1) * P, pinned=True)
+            hv = host.numpy().reshape(n + 1, P)
+            layout.pack(local, hv[0])
+            for j, x in enumerate(nbrs):
+                layout.pack(x, hv[j + 1])
+            dev = self._cached("d_in", (n + 1) * P)
+            dev.copy_(host, non_blocking=True)
+            d = dev.view(n + 1, P)
+            out = self._cached("d_out", P)
             kept = None
             if compress is not None:
                 mode, layer = compress
                 b, e = layout.segment(layer)
-                kept = self.engine.counter()
-                self.engine.mix_seq_compress(out, d_local, d_nbrs, list(alphas), mode, b, e, kept,
-                                             stream=self._stream())
+                kept = self._cached("d_cnt", 1, torch.int64)
+                kept.zero_()
+                self.engine.mix_seq_compress(out, d[0], list(d[1:]), list(alphas), mode, b, e, kept, stream=st)
             elif divisors is not None:
-                self.engine.mix_seq_div(out, d_local, d_nbrs, list(alphas), list(divisors),
-                                        stream=self._stream())
+                self.engine.mix_seq_div(out, d[0], list(d[1:]), list(alphas), list(divisors), stream=st)
             else:
-                self.engine.mix_seq(out, d_local, d_nbrs, list(alphas), stream=self._stream())
-            flat = out.cpu().numpy()
-            kept_n = int(kept.item()) if kept is not None else None
+                self.engine.mix_seq(out, d[0], list(d[1:]), list(alphas), stream=st)
+            h_out = self._cached("h_out", P, pinned=True)
+            h_out.copy_(out, non_blocking=True)
+            if kept is not None:
+                h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
+                h_cnt.copy_(kept, non_blocking=True)
+            st.synchronize()
+            flat = h_out.numpy().copy()  # the pinned buffer is reused by the next call
+            kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
     def compress(self, y: np.ndarray, ref: Optional[np.ndarray], mode: int) -> Tuple[np.ndarray, int]:

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Measurements at the functional BASELINE configs (the bench line is the 8 x 25M headline;
+these are the reference's own shapes). Prints one JSON line per config.
+
+configs[0..2] (one device's consensus call, files and protocol included, protocol sleeps off):
+    drop-in call latency (median of repeated calls) and the numpy restatement of the same
+    arithmetic (oracle, CPU) for context.
+configs[3..4] (whole population round, buckets resident in HBM): one population-kernel launch
+    (cfa_mix_population_f32) per round; algorithmic GB/s; numpy per-device loop on one core.
+"""
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["FEDERATED_AMD_PAUSE_SCALE"] = "0"
+
+import numpy as np  # noqa: E402
+import scipy.io as sio  # noqa: E402
+import torch  # noqa: E402
+
+from federated_amd import topology as T  # noqa: E402
+from federated_amd.engine import get_engine  # noqa: E402
+from oracle import cfa_oracle as O  # noqa: E402
+
+
+def med_time(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def tf1_call(shapes, K, N, module, reps=20, **kw):
+    from federated_amd.consensus import cfa, cfa_ongraphs
+    rng = np.random.default_rng(0)
+    models = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(K)]
+    old = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            if module == "cfa":
+                procs = [cfa.CFA_process(True, K, j, N) for j in range(K)]
+                for j in range(K):
+                    W1, b1, W2, b2 = models[j]
+                    procs[j].getFederatedWeight(W1, W2, b1, b2, 0, np.zeros(3), 1.0)
+                p = procs[1]
+                W1, b1, W2, b2 = models[1]
+                call = lambda: p.getFederatedWeight(W1, W2, b1, b2, 1, np.zeros(3), 1.0)
+                nbr = p.neighbor_vec
+            else:
+                procs = [cfa_ongraphs.CFA_process(True, K, j, N, 6, kw["compression"], 1) for j in range(K)]
+                for j in range(K):
+                    W1, b1, W2, b2 = models[j]
+                    procs[j].getFederatedWeight(W1, W2, b1, b2, 0, np.zeros(3), 1.0, [], False)
+                p = procs[1]
+                nbr = [0, 2, 3][:N]
+                W1, b1, W2, b2 = models[1]
+                call = lambda: p.getFederatedWeight(W1, W2, b1, b2, 1, np.zeros(3), 1.0, nbr, False)
+            call()
+            t_call = med_time(call, reps)
+            local = models[1]
+            nbrs = [models[int(j)] for j in nbr]
+            wf = [O.tf1_weight_factor(K, 1, int(j), (N - 1) if module == "cfa" else len(nbr)) for j in nbr]
+
+            def numpy_path():
+                out = O.tf1_mix(local, nbrs, 1.0, wf)
+                if module != "cfa" and kw["compression"]:
+                    O.tf1_compress(np.asarray(out[2], dtype=np.float64), local[2], kw["compression"])
+            t_np = med_time(numpy_path, reps)
+            t_io = med_time(lambda: [sio.loadmat(f"datamat{int(j)}_0.mat") for j in nbr], reps)
+        finally:
+            os.chdir(old)
+    P = sum(int(np.prod(s)) for s in shapes)
+    return {"P": P, "neighbours": len(nbr), "dropin_call_ms": round(t_call * 1e3, 3),
+            "of_which_mat_loads_ms": round(t_io * 1e3, 3), "numpy_arith_ms": round(t_np * 1e3, 3)}
+
+
+def population(D, P, lists, policy, reps=20):
+    eng = get_engine(0)
+    models = torch.randn(D, P, device="cuda")
+    pr = T.PopulationRound(eng, models)
+    pr.set_topology(lists, policy)
+    pr.run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        pr.run()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    B = sum((len(l) + 2) * P * 4 for l in lists)
+    host = models.cpu().numpy()
+
+    def numpy_round():
+        for d in range(D):
+            O.sequential_mix(host[d], [host[j] for j in lists[d]], policy(lists[d], d, D))
+    t_np = med_time(numpy_round, 2)
+    return {"devices": D, "P": P, "round_us": round(t * 1e6, 1), "GBps": round(B / t / 1e9, 1),
+            "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
+
+
+def main():
+    rows = []
+    rows.append({"config": "C1 2NN, 4 devices, cfa.py (federated_sample_2NN_CFA.py)",
+                 **tf1_call([(512, 32), (32,), (32, 8), (8,)], 4, 2, "cfa")})
+    rows.append({"config": "C2 CNN FL_CFA_CNN_tf2 shapes, 8 devices, K=3, cfa_ongraphs mode 1, compression 2",
+                 **tf1_call([(3, 3, 1, 4), (4,), (4096, 6), (6,)], 8, 3, "ongraphs", compression=2)})
+    rows.append({"config": "C3 CFA-GE CNN, 16 devices, N=2 (stage-1 mix via cfa.py math)",
+                 **tf1_call([(16, 1, 8), (8,), (168, 8), (8,)], 16, 2, "cfa")})
+    rows.append({"config": "C4 CIFAR-100 VGG-1, 32 devices, K=4 window, one population launch",
+                 **population(32, 1_071_748, [[(d + o) % 32 for o in (-2, -1, 1, 2)] for d in range(32)], T.alphas_tf2)})
+    rows.append({"config": "C5 radar CNN, 128 devices, ring (v4 N=1), one population launch",
+                 **population(128, 24_622, T.ring_v4(128, 1), T.alphas_tf2)})
+    rows.append({"config": "C5 at 25M params/device (scaling shape), 32 devices ring",
+                 **population(32, 25_000_000, T.ring_v4(32, 1), T.alphas_tf2, reps=5)})
+    for r in rows:
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
