@@ -107,8 +107,35 @@ def population(D, P, lists, policy, reps=20):
             "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
 
 
+def _cpu_worker(args):
+    seed, P, K, reps = args
+    rng = np.random.default_rng(seed)
+    local = rng.standard_normal(P, dtype=np.float32)
+    nbrs = [rng.standard_normal(P, dtype=np.float32) for _ in range(K)]
+    a = [1.0 / (K + 1)] * K
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        O.sequential_mix(local, nbrs, a)
+    return time.perf_counter() - t0
+
+
+def cpu_pool_round(P=25_000_000, K=8, workers=None, reps=3):
+    """SURVEY §8d CPU baseline (2): one process per simulated device (the reference's process
+    model, FL_CFA_CNN_tf2.py:317-319), `workers` devices mixing concurrently."""
+    import multiprocessing as mp
+    workers = workers or min(16, os.cpu_count() or 1)
+    with mp.get_context("spawn").Pool(workers) as pool:
+        t0 = time.perf_counter()
+        times = pool.map(_cpu_worker, [(i, P, K, reps) for i in range(workers)])
+        wall = time.perf_counter() - t0
+    mix_time = max(times)  # the mixing phase (data generation excluded)
+    return {"workers": workers, "P": P, "K": K, "mixes": workers * reps,
+            "aggregate_GBps": round(workers * reps * (K + 2) * P * 4 / mix_time / 1e9, 2), "wall_s": round(wall, 1)}
+
+
 def main():
     rows = []
+    rows.append({"config": "CPU pool baseline: 8 x 25M mix, one process per device", **cpu_pool_round()})
     rows.append({"config": "C1 2NN, 4 devices, cfa.py (federated_sample_2NN_CFA.py)",
                  **tf1_call([(512, 32), (32,), (32, 8), (8,)], 4, 2, "cfa")})
     rows.append({"config": "C2 CNN FL_CFA_CNN_tf2 shapes, 8 devices, K=3, cfa_ongraphs mode 1, compression 2",
