@@ -965,6 +965,46 @@ __global__ __launch_bounds__(kBlock) void mix8_gld_bst_kernel(float* out, Fanin 
     }
   }
 }
+// Traversal-order experiment: 0 = grid-stride (production), 1 = blocked (each workgroup owns a
+// contiguous span of tiles), 2 = XCD-grouped grid-stride (blocks are dispatched round-robin over
+// the 8 XCDs; the logical id is remapped so each XCD walks a contiguous run of tiles).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void mix8_trav_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const long long G = gridDim.x;
+  long long t0, t1, step;
+  if constexpr (MODE == 1) {
+    t0 = full * blockIdx.x / G;
+    t1 = full * (blockIdx.x + 1) / G;
+    step = 1;
+  } else if constexpr (MODE == 2) {
+    const long long per = G / 8;  // host guarantees G % 8 == 0
+    t0 = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    t1 = full;
+    step = G;
+  } else {
+    t0 = blockIdx.x;
+    t1 = full;
+    step = G;
+  }
+  for (long long t = t0; t < t1; t += step) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                             (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+    }
+  }
+}
 }  // namespace
 
 extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
@@ -992,4 +1032,27 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
   CFA_G(0) CFA_G(2) CFA_G(16) CFA_G(17) CFA_G(18) CFA_G(1)
 #undef CFA_G
   return fail(CFA_E_INVALID, "policy pair not instantiated");
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_traverse(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int mode, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  if (mode == 2) grid -= grid % 8;
+  if (grid == 0) return fail(CFA_E_INVALID, "experiment grid too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == 0) mix8_trav_kernel<0><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 1) mix8_trav_kernel<1><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 2) mix8_trav_kernel<2><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else return fail(CFA_E_INVALID, "unknown traversal mode");
+  return check_launch("mix8_trav");
 }
