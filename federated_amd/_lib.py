@@ -60,6 +60,12 @@ SIGNATURES = {
                                      _c_size_t, _c_void_p]),
     "cfa_mix_seq_compress_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
                                           _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_mix_tf1_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,
+                                 _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_mix_tf1_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int, _c_int,
+                                 _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_mewma_tf1_f64": (_c_int, [_c_void_p, _PP, _PP, _c_int64_p, _c_int, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, _c_size_t, _c_int, _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_compress_epilogue_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p,
                                            _c_void_p]),
     "cfa_mewma_update_f32": (_c_int, [_c_void_p, _PP, _PP, _c_int64_p, _c_int, ctypes.c_double,
@@ -133,6 +139,13 @@ def ptr_table(ptrs) -> "ctypes.Array":
 
 def float_array(vals) -> "ctypes.Array":
     arr = (ctypes.c_float * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def double_array(vals) -> "ctypes.Array":
+    arr = (ctypes.c_double * max(1, len(vals)))()
     for i, v in enumerate(vals):
         arr[i] = v
     return arr

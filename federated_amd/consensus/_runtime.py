@@ -102,12 +102,16 @@ class HostMixer:
 
     def mix(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float],
             compress: Optional[Tuple[int, int]] = None,
-            divisors: Optional[Sequence[float]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
+            divisors: Optional[Sequence[float]] = None,
+            tf1: bool = False) -> Tuple[List[np.ndarray], Optional[int]]:
         """Sequential CFA mix of the per-layer arrays ``local`` with each neighbour's per-layer
         arrays, w <- w + alphas[j] * (x_j - w) per layer, all n neighbours folded in one kernel.
         ``compress=(mode, layer)`` fuses the cfa_ongraphs compression epilogue on that layer
         (with the pre-mix local as DPCM reference) and returns the kept count.
         ``divisors`` selects the FedAvg form w <- w + (alphas[j] * (x_j - w)) / divisors[j].
+        ``tf1`` selects the TF1 numerics (``cfa_mix_tf1_f32``): ``alphas`` are the float64
+        products eps * wf_j, the chain and the epilogue run in fp64 as the reference's do under
+        numpy 2, and the result is that fp64 result rounded once to fp32.
 
         Host path: the local and all neighbour buckets are packed into ONE cached
         pinned staging buffer and moved by one async H2D copy; the result (and the kept count)
@@ -127,7 +131,16 @@ class HostMixer:
             d = dev.view(n + 1, P)
             out = self._cached("d_out", P)
             kept = None
-            if compress is not None:
+            if tf1:
+                mode, b, e = 0, 0, 0
+                if compress is not None:
+                    mode, layer = compress
+                    b, e = layout.segment(layer)
+                    kept = self._cached("d_cnt", 1, torch.int64)
+                    kept.zero_()
+                self.engine.mix_tf1(out, d[0], list(d[1:]), [float(a) for a in alphas], mode, b, e, kept,
+                                    stream=st)
+            elif compress is not None:
                 mode, layer = compress
                 b, e = layout.segment(layer)
                 kept = self._cached("d_cnt", 1, torch.int64)
@@ -184,6 +197,113 @@ class HostMixer:
             for k, arr in enumerate(layout.unpack(s_out[j], copy=False)):
                 states[k][..., j] = arr
         return layout.unpack(W_out, copy=False)
+
+    # -- TF1 on fp64 buckets: the reference's own arithmetic and dtypes -----------------------
+    @staticmethod
+    def _runs(flags):
+        """Maximal runs of consecutive tensors sharing a flag: [(first, last + 1, flag)]."""
+        runs, k = [], 0
+        while k < len(flags):
+            e = k
+            while e < len(flags) and flags[e] == flags[k]:
+                e += 1
+            runs.append((k, e, flags[k]))
+            k = e
+        return runs
+
+    def _upload64(self, layout: BucketLayout, arrays) -> torch.Tensor:
+        host = torch.from_numpy(layout.pack(arrays, np.empty(layout.P, dtype=np.float64)))
+        return host.to(self.engine.device, non_blocking=False)
+
+    def mix_tf1(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float],
+                compress: Optional[Tuple[int, int]] = None) -> Tuple[List[np.ndarray], Optional[int]]:
+        """TF1 mix with the reference's numerics and dtypes (``cfa_mix_tf1_f64``): the arrays are
+        widened to fp64 buckets (exact), folded as numpy 2 folds them (``eps * wf`` is an
+        np.float64: fp32 first subtraction when both operands are fp32 arrays, fp64 after), the
+        compression epilogue of ``compress=(mode, layer)`` applied in fp64; returns the fp64
+        arrays the reference returns, with the local shapes, and the kept count (or None).
+        Needs at least one neighbour (with none, the reference returns the inputs themselves)."""
+        n = len(nbrs)
+        if n == 0:
+            raise ValueError("mix_tf1 needs at least one neighbour model")
+        layout = BucketLayout.of(local)
+        P = layout.P
+        flags = [np.asarray(local[k]).dtype == np.float32 and np.asarray(nbrs[0][k]).dtype == np.float32
+                 for k in range(len(local))]
+        st = self._stream()
+        with torch.cuda.stream(st):
+            host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
+            hv = host.numpy().reshape(n + 1, P)
+            layout.pack(local, hv[0])
+            for j, x in enumerate(nbrs):
+                layout.pack(x, hv[j + 1])
+            dev = self._cached("d_in64", (n + 1) * P, torch.float64)
+            dev.copy_(host, non_blocking=True)
+            d = dev.view(n + 1, P)
+            out = self._cached("d_out64", P, torch.float64)
+            mode, cb, ce, kept = 0, 0, 0, None
+            if compress is not None:
+                mode, layer = compress
+                cb, ce = layout.segment(layer)
+                kept = self._cached("d_cnt", 1, torch.int64)
+                kept.zero_()
+            for k0, k1, f32 in self._runs(flags):  # one launch per run of equal step-0 precision
+                b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
+                lo, hi = max(cb, b), min(ce, e)
+                hit = kept is not None and lo < hi
+                self.engine.mix_tf1_f64(out[b:e], d[0, b:e], [d[j, b:e] for j in range(1, n + 1)],
+                                        [float(a) for a in alphas], f32, mode if hit else 0,
+                                        lo - b if hit else 0, hi - b if hit else 0,
+                                        kept if hit else None, stream=st)
+            h_out = self._cached("h_out64", P, torch.float64, pinned=True)
+            h_out.copy_(out, non_blocking=True)
+            if kept is not None:
+                h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
+                h_cnt.copy_(kept, non_blocking=True)
+            st.synchronize()
+            flat = h_out.numpy().copy()
+            kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
+        return layout.unpack(flat, copy=False), kept_n
+
+    def mewma_tf1(self, W: Sequence, states: Sequence[np.ndarray], grads: Sequence[Sequence], rho: float,
+                  lrs: Sequence[float], init: bool, use_filtered: bool) -> List[np.ndarray]:
+        """CFA-GE update with the reference's fp64 operations (``cfa_mewma_tf1_f64``): ``W``
+        (per-layer arrays), the neighbours' slot gradients ``grads[j]``, the caller's saved-state
+        arrays ``states[k]`` [..., N] updated IN PLACE at slot j in their own dtype. Every
+        operation is promoted as numpy 2 promotes it for the arrays' dtypes (Python-float rho and
+        learning rates), so the result is the reference's: fp64 model arrays for its fp64
+        gradients. ``lrs`` as in ``mewma``."""
+        layout = BucketLayout.of(W)
+        n = len(grads)
+        first_other = next((k for k in range(len(lrs)) if lrs[k] != lrs[0]), len(lrs))
+        if any(lr != lrs[-1] for lr in lrs[first_other:]):
+            raise ValueError("learning rates must be one value for the leading layers, one for the rest")
+        split = int(layout.offsets[first_other])
+        lr1, lr2 = float(lrs[0]), float(lrs[-1])
+        from ..engine import TF1_GRAD_F32, TF1_STATE_F32, TF1_W_F32
+        f32 = lambda a: np.asarray(a).dtype == np.float32
+        flags = [(TF1_STATE_F32 if f32(states[k]) else 0) | (TF1_W_F32 if f32(W[k]) else 0)
+                 | (TF1_GRAD_F32 if n and all(f32(g[k]) for g in grads) else 0) for k in range(len(W))]
+        if n and any(len({f32(g[k]) for g in grads}) > 1 for k in range(len(W))):
+            raise ValueError("neighbour gradients of one layer must share a dtype")
+        st_ = self._stream()
+        with torch.cuda.stream(st_):
+            dW = self._upload64(layout, W)
+            ds = [self._upload64(layout, [np.asarray(st)[..., j] for st in states]) for j in range(n)]
+            dg = [self._upload64(layout, g) for g in grads]
+            for k0, k1, f32 in self._runs(flags):
+                b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
+                self.engine.mewma_tf1_f64(dW[b:e], [x[b:e] for x in ds], [x[b:e] for x in dg], rho, lr1, lr2,
+                                          max(0, min(split, e) - b), init, use_filtered, f32, stream=st_)
+            W_out = dW.cpu().numpy()
+            s_out = [x.cpu().numpy() for x in ds]
+        for j in range(n):
+            for k, arr in enumerate(layout.unpack(s_out[j], copy=False)):
+                states[k][..., j] = arr
+        # a model tensor stays fp32 only while every update it receives is fp32 (or none comes)
+        u32 = lambda k: bool(flags[k] & (TF1_STATE_F32 if use_filtered else TF1_GRAD_F32))
+        return [w.astype(np.float32) if (n == 0 or (flags[k] & TF1_W_F32 and u32(k))) and f32(W[k]) else w
+                for k, w in enumerate(layout.unpack(W_out, copy=False))]
 
 
 _mixers = {}

@@ -99,8 +99,9 @@ def load_neighbour_models(nbr_vec, epoch: int, sleep_before: float = 0.0, sleep_
 
 
 def gpu_mix(local4: Sequence, nbr_models: Sequence, alphas: Sequence[float], compress=None):
-    """One GPU pass over all neighbours; returns ([W1, b1, W2, b2] fp32, kept count)."""
-    return mixer().mix(list(local4), nbr_models, alphas, compress)
+    """One GPU pass over all neighbours with the reference's TF1 numerics on fp64 buckets
+    (cfa_mix_tf1_f64); returns ([W1, b1, W2, b2] as the reference's fp64 arrays, kept count)."""
+    return mixer().mix_tf1(list(local4), nbr_models, alphas, compress)
 
 
 def publish(dev: int, ep: int, W1, b1, W2, b2, **extra) -> None:

@@ -53,7 +53,8 @@ class CFA_process:
     def getFederatedWeight(self, n_W_l1, n_W_l2, n_b_l1, n_b_l2, epoch, v_loss, eps_t_control):
         """cfa.py:105-154. Epoch 0 publishes the local model; later epochs mix the local model
         with every neighbour's epoch-1 model (sequential rule, one GPU pass), publish the PRE-mix
-        local model as datamat{ii}_{epoch}.mat and return (W1, b1, W2, b2), biases squeezed, fp32."""
+        local model as datamat{ii}_{epoch}.mat and return (W1, b1, W2, b2), biases squeezed, as the
+        reference's fp64 arrays."""
         ii = self.ii_saved_local
         if not self.federated:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)

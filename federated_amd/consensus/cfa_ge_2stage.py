@@ -4,9 +4,10 @@ CFA with gradient exchange (CFA-GE), 4-stage (``getFederatedWeight_gradients``) 
 ``federated_sample_CNN_CFA-GE.py:124-190``.
 
 Stage 1 (CFA mix of the neighbours' models) and the gradient-bucket update (MEWMA filter + SGD
-step with the neighbours' gradients) are libcfa kernels: ``cfa_mix_seq_f32`` folds all
-neighbours in one pass, ``cfa_mewma_update_f32`` applies every neighbour's gradient and
-updates every saved state in one pass ((3n + 2) * P * 4 bytes). The neighbour-gradient
+step with the neighbours' gradients) are libcfa kernels on fp64 buckets, the reference's own
+numpy-2 arithmetic: ``cfa_mix_tf1_f64`` folds all neighbours in one pass,
+``cfa_mewma_tf1_f64`` applies every neighbour's gradient and updates every saved state in one
+pass ((3n + 2) * P * 8 bytes). Outputs are the reference's fp64 arrays, bit for bit. The neighbour-gradient
 evaluation (a model forward/backward, not a reduction) runs through ``self.grad_fn``
 (default: the torch restatement of the TF1 graph in ``_tf1_models``).
 """
@@ -131,7 +132,7 @@ class CFA_ge_process:
         return states
 
     def _update(self, W4, states, grads, lr1, lr2, init, use_filtered):
-        W = mixer().mewma(W4, states, grads, self.mewma, (lr1, lr1, lr2, lr2), init, use_filtered)
+        W = mixer().mewma_tf1(W4, states, grads, self.mewma, (lr1, lr1, lr2, lr2), init, use_filtered)
         return _tf1.squeeze_out(*W)
 
     # -- 4-stage ------------------------------------------------------------------------------

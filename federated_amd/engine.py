@@ -33,19 +33,22 @@ def _require_gpu(device: Optional[torch.device]) -> torch.device:
     return torch.device("cuda", device.index if device.index is not None else torch.cuda.current_device())
 
 
-def _check_bucket(t: torch.Tensor, name: str, P: Optional[int] = None) -> int:
+def _check_bucket(t: torch.Tensor, name: str, P: Optional[int] = None, dtype=torch.float32) -> int:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if not t.is_cuda:
         raise ValueError(f"{name} must live on the GPU (got {t.device})")
-    if t.dtype != torch.float32:
-        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     n = t.numel()
     if P is not None and n != P:
         raise ValueError(f"{name} has {n} elements, expected {P}")
     return n
+
+
+TF1_STATE_F32, TF1_GRAD_F32, TF1_W_F32 = 1, 2, 4  # cfa_mewma_tf1_f64 dtype mask
 
 
 class BucketLayout:
@@ -65,7 +68,8 @@ class BucketLayout:
         return int(self.offsets[k]), int(self.offsets[k + 1])
 
     def pack(self, arrays, out: Optional[np.ndarray] = None) -> np.ndarray:
-        """Flatten per-layer arrays into ``out`` (fp32, length P), converting dtype if needed."""
+        """Flatten per-layer arrays into ``out`` (length P; fp32 unless ``out`` says otherwise),
+        converting dtype if needed."""
         if out is None:
             out = np.empty(self.P, dtype=np.float32)
         if len(arrays) != len(self.sizes):
@@ -185,6 +189,66 @@ class Engine:
                   len(nbrs), P, int(mode), int(cbegin), int(cend), kept.data_ptr(),
                   self.stream_handle(stream))
         return out
+
+    def mix_tf1(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                alphas: Sequence[float], mode: int = 0, cbegin: int = 0, cend: int = 0,
+                kept: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """TF1 mix with the reference's numpy-2 numerics (fp32 first subtraction, fp64 chain,
+        fp64 compression epilogue on [cbegin, cend), one rounding to fp32). ``alphas`` are the
+        float64 products eps * wf_j. ``kept`` (int64 CUDA tensor of one element) is required
+        when ``mode`` != 0."""
+        P = _check_bucket(local, "local")
+        _check_bucket(out, "out", P)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P)
+        if kept is not None:
+            self._check_counter(kept)
+        _lib.call("cfa_mix_tf1_f32", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas),
+                  len(nbrs), P, int(mode), int(cbegin), int(cend),
+                  kept.data_ptr() if kept is not None else None, self.stream_handle(stream))
+        return out
+
+    def mix_tf1_f64(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                    alphas: Sequence[float], step0_f32: bool, mode: int = 0, cbegin: int = 0,
+                    cend: int = 0, kept: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """TF1 mix on fp64 buckets (cfa_mix_tf1_f64): the reference's fp64 chain, unrounded.
+        ``step0_f32``: the reference's local and first-neighbour arrays are both fp32."""
+        F64 = torch.float64
+        P = _check_bucket(local, "local", dtype=F64)
+        _check_bucket(out, "out", P, F64)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P, F64)
+        if kept is not None:
+            self._check_counter(kept)
+        _lib.call("cfa_mix_tf1_f64", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas), len(nbrs),
+                  int(bool(step0_f32)), P, int(mode), int(cbegin), int(cend),
+                  kept.data_ptr() if kept is not None else None, self.stream_handle(stream))
+        return out
+
+    def mewma_tf1_f64(self, W: torch.Tensor, s: Sequence[torch.Tensor], g: Sequence[torch.Tensor],
+                      rho: float, lr1: float, lr2: float, lr_split: int, init: bool,
+                      use_filtered: bool, f32_mask: int = 0, stream=None) -> torch.Tensor:
+        """CFA-GE MEWMA on fp64 buckets (cfa_mewma_tf1_f64); W and s_j in place. ``g`` may be
+        element-strided 1-D fp64 views. ``f32_mask``: which reference arrays are fp32
+        (TF1_STATE_F32 | TF1_GRAD_F32 | TF1_W_F32)."""
+        F64 = torch.float64
+        P = _check_bucket(W, "W", dtype=F64)
+        if len(s) != len(g):
+            raise ValueError("one state bucket per gradient bucket")
+        strides = []
+        for j in range(len(g)):
+            _check_bucket(s[j], f"s[{j}]", P, F64)
+            gj = g[j]
+            if not gj.is_cuda or gj.dtype != F64 or gj.dim() != 1 or gj.numel() != P:
+                raise ValueError(f"g[{j}] must be a 1-D fp64 CUDA view of {P} elements")
+            strides.append(int(gj.stride(0)))
+        _lib.call("cfa_mewma_tf1_f64", W.data_ptr(), _lib.ptr_table([x.data_ptr() for x in s]),
+                  _lib.ptr_table([x.data_ptr() for x in g]), _lib.int64_array(strides), len(g),
+                  float(rho), float(lr1), float(lr2), int(lr_split), int(bool(init)),
+                  int(bool(use_filtered)), int(f32_mask), P, self.stream_handle(stream))
+        return W
 
     def compress(self, y: torch.Tensor, ref: Optional[torch.Tensor], mode: int,
                  kept: torch.Tensor, stream=None) -> torch.Tensor:

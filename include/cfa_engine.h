@@ -61,7 +61,11 @@ enum {
   CFA_RULE_SEQUENTIAL_DIV = 2
 };
 
-/* Compression epilogue modes (TF1/consensus/cfa_ongraphs.py:225-273). */
+/* Compression epilogue modes (TF1/consensus/cfa_ongraphs.py:225-273). The fp32 entry points
+ * (cfa_mix_seq_compress_f32, cfa_compress_epilogue_f32) evaluate them as numpy 2 does on fp32
+ * arrays: threshold and replacement cast to fp32, test / product / DPCM sum in fp32. The TF1
+ * entry points (cfa_mix_tf1_f32, cfa_mix_tf1_f64) evaluate them in fp64 on the fp64 chain, as
+ * the reference does on its promoted W_up_l2. */
 enum {
   CFA_COMPRESS_NONE = 0,
   CFA_COMPRESS_SPARSE = 1,          /* |y| < 1e-3 -> sign(y) * 1e-4                       :227-237 */
@@ -136,6 +140,56 @@ CFA_API int cfa_mix_seq_compress_f32(float* out, const float* local, const float
  * for modes 1/4). Adds the kept count to *kept_count (device uint64). */
 CFA_API int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, size_t P,
                               unsigned long long* kept_count, void* stream);
+
+/* (a1/a2/a3) TF1 mix with the reference's numpy-2 numerics, fp32 buckets in and out:
+ *   step 0:  w = (double)local + alphas[0] * (double)(x_0 - local)   (x_0 - local in fp32)
+ *   step j:  w = w + alphas[j] * ((double)x_j - w)                     (fp64)
+ *   out = (float)w after the optional compression epilogue, evaluated on the fp64 w with the
+ *   fp32 `local` as DPCM reference, on elements [cbegin, cend).
+ * In the reference, eps * wf is an np.float64, so the first subtraction is fp32 and the rest of
+ * the chain is promoted to fp64 (TF1/consensus/cfa.py:69-76, cfa_ongraphs.py:112-119 and the
+ * compression loop :225-273, cfa_mobilenet.py:82-91, cfa_ge_2stage.py:76-83). The result is
+ * the reference's fp64 result rounded once to fp32, which is what the TF1 drivers feed back
+ * into their fp32 graph. alphas[j] = eps * wf_j are host doubles. kept_count (device uint64)
+ * may be NULL only when mode == CFA_COMPRESS_NONE (no epilogue, no count); otherwise the
+ * number of elements of [cbegin, cend) NOT replaced is ADDED to it, as in
+ * cfa_mix_seq_compress_f32 (mode 0: cend - cbegin). n > CFA_MAX_FANIN chains passes through an fp64 scratch bucket
+ * (8 * P bytes, stream-ordered allocation), so the result still rounds once. */
+CFA_API int cfa_mix_tf1_f32(float* out, const float* local, const float* const* nbrs,
+                            const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                            size_t cend, unsigned long long* kept_count, void* stream);
+
+/* (a1-a4) TF1 mix on fp64 buckets: the reference's own TF1 arithmetic, with no rounding to fp32.
+ * Under numpy 2 the reference's chain is fp64 (eps * wf is an np.float64) over whatever arrays
+ * the caller and the .mat files hold, and it returns fp64 arrays. The buckets here are those
+ * arrays widened to fp64 (exact for fp32 values):
+ *   step 0:  w = local + alphas[0] * d,  d = step0_f32 ? (double)((float)x_0 - (float)local)
+ *                                                     : x_0 - local
+ *   step j:  w = w + alphas[j] * (x_j - w)
+ * step0_f32 = 1 when the reference's local and first-neighbour arrays are both fp32 (numpy
+ * subtracts them in fp32). The optional compression epilogue (cfa_ongraphs.py:225-273) is
+ * applied in fp64 on [cbegin, cend) with `local` as DPCM reference; kept_count as in
+ * cfa_mix_tf1_f32. Replaces TF1/consensus/cfa.py:69-76, cfa_ongraphs.py:112-119 + 225-273,
+ * cfa_mobilenet.py:82-91, cfa_ge_2stage.py:76-83 (stage 1 of CFA-GE). */
+CFA_API int cfa_mix_tf1_f64(double* out, const double* local, const double* const* nbrs,
+                            const double* alphas, int n, int step0_f32, size_t P, int mode,
+                            size_t cbegin, size_t cend, unsigned long long* kept_count,
+                            void* stream);
+
+/* (a4) CFA-GE MEWMA on fp64 buckets with the reference's numpy-2 operations
+ * (cfa_ge_2stage.py:331-371, :593-621), for j = 0..n-1 in order:
+ *   s_j <- init ? g_j : rho*g_j + (1-rho)*s_j
+ *   W   <- W - lr(i) * (use_filtered ? s_j : g_j),  lr(i) = i < lr_split ? lr1 : lr2
+ * The buckets hold the reference's arrays widened to fp64; f32_mask says which of them are fp32
+ * arrays there (CFA_TF1_*_F32). rho, 1-rho and lr are Python floats in the reference, so each
+ * product is computed in its array's dtype, a sum/difference is fp32 only when both operands
+ * are, and a state is rounded to its array's dtype on store (as numpy's slice assignment does).
+ * W and s_j are updated in place; g_j is read with element stride g_stride (NULL = all 1). */
+enum { CFA_TF1_STATE_F32 = 1, CFA_TF1_GRAD_F32 = 2, CFA_TF1_W_F32 = 4 };
+CFA_API int cfa_mewma_tf1_f64(double* W, double* const* s, const double* const* g,
+                              const int64_t* g_stride, int n, double rho, double lr1, double lr2,
+                              size_t lr_split, int init, int use_filtered, int f32_mask, size_t P,
+                              void* stream);
 
 /* (a4) CFA-GE gradient-bucket update (MEWMA), for j = 0..n-1 in order:
  *   s_j <- init ? g_j : rho*g_j + (1-rho)*s_j

@@ -119,6 +119,16 @@ def tf1_mix(local4, nbr4_list, eps: float, factors) -> list:
     return [np.asarray(w[0]), np.squeeze(np.asarray(w[1])), np.asarray(w[2]), np.squeeze(np.asarray(w[3]))]
 
 
+def tf1_mix_flat(local: np.ndarray, nbrs, alphas) -> np.ndarray:
+    """tf1_mix on one flat fp32 bucket: w <- w + a_j*(x_j - w) with a_j = eps*wf_j an
+    np.float64 (cfa.py:69-76): the first subtraction is fp32, everything after it fp64.
+    Returns the fp64 (or, with no neighbour, the fp32 input) result as the reference does."""
+    w = np.asarray(local)
+    for x, a in zip(nbrs, alphas):
+        w = w + np.float64(a) * (np.asarray(x) - w)
+    return w
+
+
 COMPRESSION = {  # cfa_ongraphs.py:227-271: (threshold, replacement, differential)
     1: (0.001, 0.0001, False),
     2: (1.e-4, 1.e-4, True),

@@ -1,8 +1,9 @@
 """GPU parity of the libcfa kernels against the CPU oracle, called through the C-ABI.
 
 Bars: the sequential rule is bit-exact against fp32 numpy (same three roundings);
-the linear closed form and the fp64-reference TF1 paths are within 1e-5 normwise
-(max|y - r| <= 1e-5 * max|r|); compression counts are exact integers."""
+the TF1 rule (cfa_mix_tf1_f32) is bit-exact against the fp64 reference chain rounded once to
+fp32; the linear closed form is within 1e-5 normwise (max|y - r| <= 1e-5 * max|r|);
+compression counts are exact integers."""
 import numpy as np
 import pytest
 import torch
@@ -97,13 +98,32 @@ def test_mix_strided_gradient_slices(gpu):
 
 
 def _compress_expect(local, nbrs, alphas, mode, cb, ce):
-    y = O.sequential_mix(local, nbrs, alphas).astype(np.float32)
-    seg = y[cb:ce].astype(np.float64).reshape(-1, 6)  # W2 is [4096, 6]
-    cnt = O.tf1_compress(seg, local[cb:ce].astype(np.float64).reshape(-1, 6), mode)
-    seg = seg.reshape(-1)
-    y = y.copy()
-    y[cb:ce] = seg.astype(np.float32)
+    """fp32 chain, then the epilogue as numpy 2 evaluates it on fp32 arrays (threshold and
+    replacement cast to fp32; W2 is [4096, 6])."""
+    y = O.sequential_mix(local, nbrs, alphas).astype(np.float32).copy()
+    seg = y[cb:ce].reshape(-1, 6)
+    cnt = O.tf1_compress(seg, local[cb:ce].reshape(-1, 6), mode)
+    y[cb:ce] = seg.reshape(-1)
     return y, cnt
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_compress_fp32_threshold_boundaries(gpu, mode):
+    """fp32(0.01) < 0.01 and fp32(1e-4) < 1e-4 in exact arithmetic, but numpy 2 compares an fp32
+    array with a Python float in fp32: the boundary values are kept, not replaced."""
+    thr = {1: 1e-3, 2: 1e-4, 3: 1e-3, 4: 1e-2}[mode]
+    t32 = np.float32(thr)
+    edge = np.array([t32, -t32, np.nextafter(t32, np.float32(0)), -np.nextafter(t32, np.float32(0)),
+                     np.nextafter(t32, np.float32(1)), 0.0, -0.0, 5e-5, -5e-5, 0.5] * 6, dtype=np.float32)
+    ref = (np.arange(edge.size, dtype=np.float32) * np.float32(1e-3)) if mode in (2, 3) else None
+    y = edge + ref if ref is not None else edge.copy()
+    expect = y.copy().reshape(-1, 6)
+    cnt = O.tf1_compress(expect, (ref if ref is not None else y).reshape(-1, 6), mode)
+    dy = _dev(y)
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.compress(dy, _dev(ref) if ref is not None else None, mode, kept)
+    assert np.array_equal(dy.cpu().numpy(), expect.reshape(-1)), mode
+    assert int(kept.item()) == cnt
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
@@ -126,6 +146,163 @@ def test_mix_seq_compress(gpu, mode, n):
         assert 0 < cnt < ce - cb  # the regime exercises both branches
     elif mode in (2, 3) and not n:
         assert cnt == 0  # DPCM with no neighbour: y == ref everywhere (cfa_ongraphs.py:218-249)
+
+
+# ---- TF1 numerics (cfa_mix_tf1_f32): fp64 chain, one rounding; bit-exact vs fp32(reference) ----
+def _tf1_alphas(n, eps=0.7, devices=8):
+    return [eps * O.tf1_weight_factor(devices, 1, j % devices, max(n - 1, 0)) for j in range(n)]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 33])
+def test_mix_tf1_bitexact(gpu, n):
+    rng = np.random.default_rng(700 + n)
+    alphas = _tf1_alphas(n)
+    for P in [1, 3, 4, 5, 1023, 24_622, 1 << 20]:
+        local = _rand(rng, 1, P)[0]
+        nbrs = _rand(rng, n, P)
+        ref = O.tf1_mix_flat(local, nbrs, alphas)
+        assert ref.dtype == np.float64
+        out = torch.empty(P, dtype=torch.float32, device="cuda")
+        gpu.mix_tf1(out, _dev(local), [_dev(x) for x in nbrs], alphas)
+        assert np.array_equal(out.cpu().numpy(), ref.astype(np.float32)), (n, P)
+
+
+@pytest.mark.parametrize("offsets", [(1, 1, 1), (3, 3, 3), (0, 1, 2)])
+def test_mix_tf1_misaligned_and_inplace(gpu, offsets):
+    rng = np.random.default_rng(17)
+    P, n = 50_001, 3
+    alphas = _tf1_alphas(n, 1.0)
+    local = _rand(rng, 1, P)[0]
+    nbrs = _rand(rng, n, P)
+    ref = O.tf1_mix_flat(local, nbrs, alphas).astype(np.float32)
+    base = [_dev(np.zeros(P + 8, np.float32)) for _ in range(2)]
+    o_out, o_loc, o_nb = offsets
+    out, loc = base[0][o_out:o_out + P], base[1][o_loc:o_loc + P]
+    loc.copy_(_dev(local))
+    nb0 = _dev(np.zeros(P + 8, np.float32))[o_nb:o_nb + P]
+    nb0.copy_(_dev(nbrs[0]))
+    gpu.mix_tf1(out, loc, [nb0] + [_dev(x) for x in nbrs[1:]], alphas)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    w = _dev(local)
+    gpu.mix_tf1(w, w, [_dev(x) for x in nbrs], alphas)  # out aliases local
+    assert np.array_equal(w.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n", [0, 1, 3, 17])
+def test_mix_tf1_compress(gpu, mode, n):
+    """Fused fp64 epilogue: the reference compresses its fp64 W_up_l2 against the fp32 n_W_l2
+    (cfa_ongraphs.py:225-273); the test and replacement in fp64, the count exact."""
+    rng = np.random.default_rng(900 + 10 * mode + n)
+    P = 24_622
+    cb, ce = 40, 40 + 24_576
+    base = (rng.standard_normal(P) * 0.01).astype(np.float32)
+    local = base + (rng.standard_normal(P) * 3e-4).astype(np.float32)
+    nbrs = [base + (rng.standard_normal(P) * 3e-4).astype(np.float32) for _ in range(n)]
+    alphas = [0.9 / (n + 1) * 2] * n
+    y = O.tf1_mix_flat(local, nbrs, alphas)
+    y = y.astype(np.float64) if n else y.copy()
+    seg = y[cb:ce].reshape(-1, 6)
+    cnt = O.tf1_compress(seg, local[cb:ce].reshape(-1, 6), mode)
+    y[cb:ce] = seg.reshape(-1)
+    out = torch.empty(P, dtype=torch.float32, device="cuda")
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.mix_tf1(out, _dev(local), [_dev(x) for x in nbrs], alphas, mode, cb, ce, kept)
+    assert np.array_equal(out.cpu().numpy(), y.astype(np.float32)), (mode, n)
+    assert int(kept.item()) == cnt  # mode 0: the whole range (counter_param = W2 size)
+    if mode in (1, 2, 4) and (n or mode in (1, 4)):
+        assert 0 < cnt < ce - cb
+
+
+# ---- fp64 buckets (cfa_mix_tf1_f64 / cfa_mewma_tf1_f64): the reference's dtypes and values ----
+def _dev64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 16, 17, 40])
+@pytest.mark.parametrize("dtypes", ["f32", "f64", "local64"])
+def test_mix_tf1_f64_identical(gpu, n, dtypes):
+    """Any mix of fp32/fp64 reference arrays: identical to numpy's result, dtype included."""
+    rng = np.random.default_rng(1100 + n)
+    P = 30_011
+    alphas = _tf1_alphas(n)
+    local = _rand(rng, 1, P)[0]
+    nbrs = _rand(rng, n, P)
+    if dtypes == "f64":
+        local, nbrs = rng.standard_normal(P), [rng.standard_normal(P) for _ in range(n)]
+    elif dtypes == "local64":
+        local = local.astype(np.float64) * (1 + 1e-9)
+    ref = O.tf1_mix_flat(local, nbrs, alphas)
+    assert ref.dtype == np.float64
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    step0_f32 = local.dtype == np.float32 and nbrs[0].dtype == np.float32
+    gpu.mix_tf1_f64(out, _dev64(local), [_dev64(x) for x in nbrs], alphas, step0_f32)
+    assert np.array_equal(out.cpu().numpy(), ref), (n, dtypes)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+def test_mix_tf1_f64_compress(gpu, mode):
+    rng = np.random.default_rng(1200 + mode)
+    P, n = 24_622, 3
+    cb, ce = 40, 40 + 24_576
+    base = (rng.standard_normal(P) * 0.01).astype(np.float32)
+    local = base + (rng.standard_normal(P) * 3e-4).astype(np.float32)
+    nbrs = [base + (rng.standard_normal(P) * 3e-4).astype(np.float32) for _ in range(n)]
+    alphas = [0.45] * n
+    y = O.tf1_mix_flat(local, nbrs, alphas)
+    seg = y[cb:ce].reshape(-1, 6)
+    cnt = O.tf1_compress(seg, local[cb:ce].reshape(-1, 6), mode)
+    y[cb:ce] = seg.reshape(-1)
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.mix_tf1_f64(out, _dev64(local), [_dev64(x) for x in nbrs], alphas, True, mode, cb, ce, kept)
+    assert np.array_equal(out.cpu().numpy(), y)
+    assert int(kept.item()) == cnt
+
+
+@pytest.mark.parametrize("filtered,init", [(True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("dtypes", ["s64_g64_w64", "s32_g64_w64", "s64_g32_w64", "s32_g32_w32", "s32_g32_w64"])
+def test_mewma_tf1_f64_identical(gpu, filtered, init, dtypes):
+    """cfa_ge_2stage.py:331-371 / :593-621 on the reference's arrays, every dtype combination
+    numpy 2 can meet: the driver's fp64 saved states (np.zeros) and fp64 datagrad gradients, and
+    fp32 variants of each; the result equals numpy's, dtype included."""
+    from federated_amd.engine import TF1_GRAD_F32, TF1_STATE_F32, TF1_W_F32
+    rng = np.random.default_rng(1300)
+    shapes = [(16, 1, 8), (8,), (168, 8), (8,)]
+    n, rho, lr1, lr2 = 3, 0.99, 0.025, 0.001
+    dt = {"32": np.float32, "64": np.float64}
+    sd, gd, wd = dt[dtypes[1:3]], dt[dtypes[5:7]], dt[dtypes[9:11]]
+    state_dtype = sd
+    W4 = [rng.standard_normal(s).astype(wd) for s in shapes]
+    st4 = [rng.standard_normal(s + (n,)).astype(sd) for s in shapes]
+    g = [[rng.standard_normal(s).astype(gd) for s in shapes] for _ in range(n)]
+    mask = (TF1_STATE_F32 if sd == np.float32 else 0) | (TF1_GRAD_F32 if gd == np.float32 else 0) | \
+        (TF1_W_F32 if wd == np.float32 else 0)
+    ref_states = [x.copy() for x in st4]
+    ref_W = O.tf1_mewma([w.copy() for w in W4], ref_states, g, rho, lr1, lr2, filtered, init)
+    from federated_amd.engine import BucketLayout
+    lay = BucketLayout([s for s in shapes])
+    dW = _dev64(lay.pack(W4, np.empty(lay.P)))
+    ds = [_dev64(lay.pack([x[..., j] for x in st4], np.empty(lay.P))) for j in range(n)]
+    dg = [_dev64(lay.pack(gj, np.empty(lay.P))) for gj in g]
+    gpu.mewma_tf1_f64(dW, ds, dg, rho, lr1, lr2, int(lay.offsets[2]), init, filtered, mask)
+    for k, (a, r) in enumerate(zip(lay.unpack(dW.cpu().numpy()), ref_W)):
+        assert np.array_equal(a.astype(r.dtype), r) and np.array_equal(a, r.astype(np.float64)), (k, r.dtype)
+    for j in range(n):
+        for k, a in enumerate(lay.unpack(ds[j].cpu().numpy())):
+            assert np.array_equal(a.astype(state_dtype), ref_states[k][..., j]), (j, k)
+            assert np.array_equal(a, ref_states[k][..., j].astype(np.float64)), (j, k)
+
+
+def test_mix_tf1_error_paths(gpu):
+    from federated_amd._lib import CFAError
+    x = torch.zeros(16, device="cuda")
+    with pytest.raises(CFAError):
+        gpu.mix_tf1(x, x, [x], [0.5])  # out aliases a neighbour
+    with pytest.raises(CFAError):
+        gpu.mix_tf1(x, torch.zeros(16, device="cuda"), [torch.zeros(16, device="cuda")], [0.5], 2, 0, 8)  # no kept
+    with pytest.raises(CFAError):
+        gpu.mix_tf1(x, torch.zeros(16, device="cuda"), [], [], 9, 0, 8, torch.zeros(1, dtype=torch.int64, device="cuda"))
 
 
 @pytest.mark.parametrize("filtered,init", [(True, False), (False, False), (False, True)])
