@@ -31,6 +31,7 @@ CFA_UNIQUE_ID_BYTES = 128
 RULE_SEQUENTIAL = 0
 RULE_LINEAR = 1
 RULE_SEQUENTIAL_DIV = 2
+RULE_ACCUMULATE = 3
 
 COMPRESS_NONE = 0
 COMPRESS_SPARSE = 1
@@ -64,6 +65,8 @@ SIGNATURES = {
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int, _c_int,
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_fold_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double),
+                              ctypes.POINTER(ctypes.c_double), _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_mewma_tf1_f64": (_c_int, [_c_void_p, _PP, _PP, _c_int64_p, _c_int, ctypes.c_double, ctypes.c_double,
                                    ctypes.c_double, _c_size_t, _c_int, _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_compress_epilogue_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p,

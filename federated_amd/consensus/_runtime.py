@@ -265,6 +265,31 @@ class HostMixer:
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
+    def fold64(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float], rule: int,
+               divisors: Optional[Sequence[float]] = None) -> List[np.ndarray]:
+        """fp64 fold (``cfa_fold_f64``) of per-layer arrays widened to fp64 buckets; returns fp64
+        arrays with the local shapes. One H2D of all buckets, one launch, one D2H."""
+        layout = BucketLayout.of(local)
+        P, n = layout.P, len(nbrs)
+        st = self._stream()
+        with torch.cuda.stream(st):
+            host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
+            hv = host.numpy().reshape(n + 1, P)
+            layout.pack(local, hv[0])
+            for j, x in enumerate(nbrs):
+                layout.pack(x, hv[j + 1])
+            dev = self._cached("d_in64", (n + 1) * P, torch.float64)
+            dev.copy_(host, non_blocking=True)
+            d = dev.view(n + 1, P)
+            out = self._cached("d_out64", P, torch.float64)
+            self.engine.fold_f64(out, d[0], [d[j] for j in range(1, n + 1)], [float(a) for a in alphas], rule,
+                                 None if divisors is None else [float(x) for x in divisors], stream=st)
+            h_out = self._cached("h_out64", P, torch.float64, pinned=True)
+            h_out.copy_(out, non_blocking=True)
+            st.synchronize()
+            flat = h_out.numpy().copy()
+        return layout.unpack(flat, copy=False)
+
     def mewma_tf1(self, W: Sequence, states: Sequence[np.ndarray], grads: Sequence[Sequence], rho: float,
                   lrs: Sequence[float], init: bool, use_filtered: bool) -> List[np.ndarray]:
         """CFA-GE update with the reference's fp64 operations (``cfa_mewma_tf1_f64``): ``W``

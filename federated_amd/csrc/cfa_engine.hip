@@ -432,11 +432,16 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_scalar_kernel(void* out, int t
 struct F64Fanin {
   const double* src[CFA_MAX_FANIN + 1];  // [0] = running w (local or previous pass), [1..m]
   double a[CFA_MAX_FANIN + 1];
+  double d[CFA_MAX_FANIN + 1];           // SEQUENTIAL_DIV divisors
   int m;
 };
+// rule: CFA_RULE_SEQUENTIAL  w = w + a*(x - w)
+//       CFA_RULE_SEQUENTIAL_DIV  w = w + (a*(x - w))/d
+//       CFA_RULE_ACCUMULATE  w = w + a*x
 __global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fanin f, long long P,
-                                                             int step0_f32, const double* ref,
-                                                             CompressParams cp, int compress) {
+                                                             int rule, int step0_f32,
+                                                             const double* ref, CompressParams cp,
+                                                             int compress) {
   unsigned kept = 0;
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
        i += (long long)gridDim.x * kBlock) {
@@ -447,7 +452,13 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fan
       w = w + f.a[1] * (double)d;
       j = 2;
     }
-    for (; j <= f.m; ++j) w = w + f.a[j] * (f.src[j][i] - w);
+    if (rule == CFA_RULE_SEQUENTIAL) {
+      for (; j <= f.m; ++j) w = w + f.a[j] * (f.src[j][i] - w);
+    } else if (rule == CFA_RULE_SEQUENTIAL_DIV) {
+      for (; j <= f.m; ++j) w = w + (f.a[j] * (f.src[j][i] - w)) / f.d[j];
+    } else {
+      for (; j <= f.m; ++j) w = w + f.a[j] * f.src[j][i];
+    }
     if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one_d(w, ref[i], cp, kept);
     out[i] = w;
   }
@@ -1096,12 +1107,17 @@ extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* cons
   return rc;
 }
 
-extern "C" int cfa_mix_tf1_f64(double* out, const double* local, const double* const* nbrs,
-                               const double* alphas, int n, int step0_f32, size_t P, int mode,
-                               size_t cbegin, size_t cend, unsigned long long* kept_count,
-                               void* stream) {
+namespace {
+int fold_f64(double* out, const double* local, const double* const* nbrs, const double* alphas,
+             const double* divisors, int n, int rule, int step0_f32, size_t P, int mode,
+             size_t cbegin, size_t cend, unsigned long long* kept_count, hipStream_t st) {
   if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
   if (n > 0 && (!alphas || !nbrs)) return fail(CFA_E_INVALID, "null alphas/neighbour table");
+  if (rule == CFA_RULE_SEQUENTIAL_DIV && n > 0 && !divisors) return fail(CFA_E_INVALID, "null divisors");
+  if (rule != CFA_RULE_SEQUENTIAL && rule != CFA_RULE_SEQUENTIAL_DIV && rule != CFA_RULE_ACCUMULATE)
+    return fail(CFA_E_INVALID, "rule %d has no fp64 fold", rule);
+  if (step0_f32 && rule != CFA_RULE_SEQUENTIAL)
+    return fail(CFA_E_INVALID, "step0_f32 applies to the sequential rule only");
   if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "null kept_count");
   if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
   CompressParams cp{};
@@ -1119,11 +1135,10 @@ extern "C" int cfa_mix_tf1_f64(double* out, const double* local, const double* c
   cp.cbegin = (long long)cbegin;
   cp.cend = (long long)cend;
   cp.kept = kept_count;
-  hipStream_t st = (hipStream_t)stream;
   const unsigned grid = grid_for(((long long)P + kBlock - 1) / kBlock);
   int done = 0;
   const double* w = local;
-  do {
+  do {  // n == 0 runs one pass that copies local (and applies the epilogue)
     const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
     const bool last = done + m == n;
     F64Fanin f{};
@@ -1132,14 +1147,32 @@ extern "C" int cfa_mix_tf1_f64(double* out, const double* local, const double* c
     for (int j = 0; j < m; ++j) {
       f.src[j + 1] = nbrs[done + j];
       f.a[j + 1] = alphas[done + j];
+      f.d[j + 1] = divisors ? divisors[done + j] : 1.0;
     }
-    mix_tf1_f64_kernel<<<grid, kBlock, 0, st>>>(out, f, (long long)P, done == 0 ? step0_f32 : 0,
-                                                local, cp, last ? compress : 0);
-    if (int rc = check_launch("mix_tf1_f64")) return rc;
+    mix_tf1_f64_kernel<<<grid, kBlock, 0, st>>>(out, f, (long long)P, rule,
+                                                done == 0 ? step0_f32 : 0, local, cp,
+                                                last ? compress : 0);
+    if (int rc = check_launch("fold_f64")) return rc;
     done += m;
     w = out;
   } while (done < n);
   return CFA_OK;
+}
+}  // namespace
+
+extern "C" int cfa_mix_tf1_f64(double* out, const double* local, const double* const* nbrs,
+                               const double* alphas, int n, int step0_f32, size_t P, int mode,
+                               size_t cbegin, size_t cend, unsigned long long* kept_count,
+                               void* stream) {
+  return fold_f64(out, local, nbrs, alphas, nullptr, n, CFA_RULE_SEQUENTIAL, step0_f32, P, mode,
+                  cbegin, cend, kept_count, (hipStream_t)stream);
+}
+
+extern "C" int cfa_fold_f64(double* out, const double* local, const double* const* nbrs,
+                            const double* alphas, const double* divisors, int n, int rule,
+                            size_t P, void* stream) {
+  return fold_f64(out, local, nbrs, alphas, divisors, n, rule, 0, P, CFA_COMPRESS_NONE, 0, 0,
+                  nullptr, (hipStream_t)stream);
 }
 
 extern "C" int cfa_mewma_tf1_f64(double* W, double* const* s, const double* const* g,

@@ -227,6 +227,21 @@ class Engine:
                   kept.data_ptr() if kept is not None else None, self.stream_handle(stream))
         return out
 
+    def fold_f64(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                 alphas: Sequence[float], rule: int, divisors: Optional[Sequence[float]] = None,
+                 stream=None) -> torch.Tensor:
+        """fp64 fold (cfa_fold_f64): SEQUENTIAL, SEQUENTIAL_DIV (``divisors``) or ACCUMULATE."""
+        F64 = torch.float64
+        P = _check_bucket(local, "local", dtype=F64)
+        _check_bucket(out, "out", P, F64)
+        for j, x in enumerate(nbrs):
+            _check_bucket(x, f"nbrs[{j}]", P, F64)
+        _lib.call("cfa_fold_f64", out.data_ptr(), local.data_ptr(),
+                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas),
+                  _lib.double_array(divisors) if divisors is not None else None, len(nbrs), int(rule), P,
+                  self.stream_handle(stream))
+        return out
+
     def mewma_tf1_f64(self, W: torch.Tensor, s: Sequence[torch.Tensor], g: Sequence[torch.Tensor],
                       rho: float, lr1: float, lr2: float, lr_split: int, init: bool,
                       use_filtered: bool, f32_mask: int = 0, stream=None) -> torch.Tensor:

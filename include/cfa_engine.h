@@ -58,7 +58,9 @@ enum {
   /* Linear combination: out = c_0 * local + sum_j c_{j+1} * x_j (fp32 FMA chain). */
   CFA_RULE_LINEAR = 1,
   /* Sequential rule with a divisor: w <- w + (a_j * (x_j - w)) / d_j (FedAvg form). */
-  CFA_RULE_SEQUENTIAL_DIV = 2
+  CFA_RULE_SEQUENTIAL_DIV = 2,
+  /* Accumulation: w <- w + a_j * x_j, one rounding per product and per sum (fp64 fold only). */
+  CFA_RULE_ACCUMULATE = 3
 };
 
 /* Compression epilogue modes (TF1/consensus/cfa_ongraphs.py:225-273). The fp32 entry points
@@ -175,6 +177,21 @@ CFA_API int cfa_mix_tf1_f64(double* out, const double* local, const double* cons
                             const double* alphas, int n, int step0_f32, size_t P, int mode,
                             size_t cbegin, size_t cend, unsigned long long* kept_count,
                             void* stream);
+
+/* (f1) fp64 fold of the reference's server-side chains, on fp64 buckets (fp32 arrays widened
+ * exactly), one fp64 rounding per operation, w0 = local:
+ *   CFA_RULE_SEQUENTIAL      w <- w + alphas[j] * (x_j - w)
+ *   CFA_RULE_SEQUENTIAL_DIV  w <- w + (alphas[j] * (x_j - w)) / divisors[j]
+ *   CFA_RULE_ACCUMULATE      w <- w + alphas[j] * x_j
+ * Replaces the aggregation loops embedded in the reference's drivers, whose operands are fp64:
+ *   TF2/FL_over_MQTT/PS_server.py:130-133 (SEQUENTIAL_DIV over the decoded fp64 payloads),
+ *   TF2/FL_over_MQTT/learner_consensus.py:151-152 (SEQUENTIAL_DIV, u = 1, C = 2),
+ *   TF1/federated_sample_CNN_CFA_FA.py:86-89 (ACCUMULATE from zeros, a = 1/devices),
+ *   :103-110 and :130-133 (SEQUENTIAL, a = eps/devices), :280-283 (client, SEQUENTIAL, a = eps2).
+ * `divisors` is read only by SEQUENTIAL_DIV. out may alias local. */
+CFA_API int cfa_fold_f64(double* out, const double* local, const double* const* nbrs,
+                         const double* alphas, const double* divisors, int n, int rule, size_t P,
+                         void* stream);
 
 /* (a4) CFA-GE MEWMA on fp64 buckets with the reference's numpy-2 operations
  * (cfa_ge_2stage.py:331-371, :593-621), for j = 0..n-1 in order:

@@ -251,3 +251,53 @@ def ps_fedavg(params, models, update_factor, divide: bool = True) -> list:
             else:
                 p[q] = p[q] + update_factor * (models[k][q] - p[q])
     return p
+
+
+# ----------------------------------------------------------------------------------------
+# f1: aggregation loops embedded in the reference's drivers
+# ----------------------------------------------------------------------------------------
+def ps_mqtt_aggregate(model_parameters, local_models_storage, active_device_indexes, update_factor, active):
+    """TF2/FL_over_MQTT/PS_server.py:130-133."""
+    mp = list(model_parameters)
+    for q in range(len(mp)):
+        for k in range(active):
+            mp[q] = mp[q] + update_factor * (local_models_storage[active_device_indexes[k]][q] - mp[q]) / active
+    return mp
+
+
+def learner_consensus_mix(model_parameters, rx_global_model, update_factor=1, active=2):
+    """TF2/FL_over_MQTT/learner_consensus.py:151-152."""
+    mp = list(model_parameters)
+    for q in range(len(mp)):
+        mp[q] = mp[q] + update_factor * (rx_global_model[q] - mp[q]) / active
+    return mp
+
+
+_KEYS4 = ("weights1", "biases1", "weights2", "biases2")
+
+
+def cfa_fa_server_init(server4, contents, balancing_vect):
+    """TF1/federated_sample_CNN_CFA_FA.py:86-89, devices in order."""
+    s = list(server4)
+    for d, c in enumerate(contents):
+        for k, key in enumerate(_KEYS4):
+            s[k] = s[k] + balancing_vect[d] * c[key]
+    return s
+
+
+def cfa_fa_server_round(server4, contents, eps_t_control, balancing_vect):
+    """TF1/federated_sample_CNN_CFA_FA.py:130-133 (same as :103-110), devices in order."""
+    s = list(server4)
+    for d, c in enumerate(contents):
+        for k, key in enumerate(_KEYS4):
+            s[k] = s[k] + eps_t_control * balancing_vect[d] * (c[key] - s[k])
+    return s
+
+
+def cfa_fa_client_mix(W_val_l1, b_val_l1, W_val_l2, b_val_l2, mathcontent, eps_t_control2):
+    """TF1/federated_sample_CNN_CFA_FA.py:280-283."""
+    W_val_l1 = W_val_l1 + eps_t_control2 * (np.asarray(mathcontent['weights1']) - W_val_l1)
+    b_val_l1 = b_val_l1 + eps_t_control2 * (np.squeeze(np.asarray(mathcontent['biases1'])) - b_val_l1)
+    W_val_l2 = W_val_l2 + eps_t_control2 * (np.array(mathcontent['weights2']) - W_val_l2)
+    b_val_l2 = b_val_l2 + eps_t_control2 * (np.squeeze(np.asarray(mathcontent['biases2'])) - b_val_l2)
+    return W_val_l1, b_val_l1, W_val_l2, b_val_l2

@@ -576,6 +576,112 @@ def case_parameter_server():
     save("tf2_parameter_server.npz", **out)
 
 
+# --------------------------------------------------------------------------------------
+# f1: aggregation loops embedded in drivers (PS_server.py, learner_consensus.py,
+# federated_sample_CNN_CFA_FA.py). The drivers cannot be imported (argparse at import, TF
+# graphs, MQTT sockets), so the cited statements are read from the driver files and executed as
+# they stand, in a namespace holding the variables they use.
+# --------------------------------------------------------------------------------------
+def driver_block(path: str, first: str, last: str, after: str = None):
+    """Dedented source of the driver lines from the first line containing ``first`` (after the
+    line containing ``after``) through the next line containing ``last``; returns (code, lines)."""
+    import textwrap
+    with open(path) as f:
+        lines = f.read().splitlines()
+    start = 0
+    if after is not None:
+        start = next(i for i, l in enumerate(lines) if after in l)
+    i = next(k for k in range(start, len(lines)) if first in lines[k])
+    j = next(k for k in range(i, len(lines)) if last in lines[k])
+    return textwrap.dedent("\n".join(lines[i:j + 1])), (i + 1, j + 1)
+
+
+def mat_roundtrip(model4):
+    """What sio.loadmat returns for a datamat written by savemat (1-D biases come back [1, n])."""
+    with Workdir():
+        sio.savemat("m.mat", dict(zip(("weights1", "biases1", "weights2", "biases2"), model4)))
+        c = sio.loadmat("m.mat")
+    return {k: c[k] for k in ("weights1", "biases1", "weights2", "biases2")}
+
+
+def case_driver_aggregations():
+    out = {}
+    rng = np.random.default_rng(4242)
+    # ---- MQTT PS (PS_server.py:130-133) and device-side mix (learner_consensus.py:151-152)
+    ps_path = os.path.join(TF2, "FL_over_MQTT", "PS_server.py")
+    lc_path = os.path.join(TF2, "FL_over_MQTT", "learner_consensus.py")
+    code_ps, span_ps = driver_block(ps_path, "for q in range(layers):", "/ active",
+                                    after="active_device_indexes = indexes_tx[:, epoch_count]")
+    code_lc, span_lc = driver_block(lc_path, "for q in range(layers):", "/ active", after="# apply consensus")
+    out["ps_mqtt/src_lines"] = np.array(span_ps)
+    out["learner/src_lines"] = np.array(span_lc)
+    D, layers = 6, len(SHAPES_LENET1)
+    glob_ = gen_model(rng, SHAPES_LENET1)  # model_global.get_weights(): fp32
+    # payload layers: ndarray.tolist() on the learner, np.asarray(list) on the server -> fp64
+    storage = [[np.asarray(a.tolist()) for a in gen_model(rng, SHAPES_LENET1)] for _ in range(D)]
+    idx = rng.permutation(D)
+    for t in range(layers):
+        out[f"ps_mqtt/global_{t}"] = glob_[t]
+        out[f"ps_mqtt/storage_{t}"] = np.stack([m[t] for m in storage])
+    out["ps_mqtt/idx"] = idx
+    for tag, active, u in (("a4_u1", 4, 1), ("a1_u05", 1, 0.5), ("a6_u1", 6, 1)):
+        ns = {"layers": layers, "active": active, "update_factor": u, "local_models_storage": storage,
+              "active_device_indexes": idx, "model_parameters": [a.copy() for a in glob_]}
+        exec(code_ps, ns)
+        for t in range(layers):
+            out[f"ps_mqtt/{tag}/out_{t}"] = np.asarray(ns["model_parameters"][t])
+        out[f"ps_mqtt/{tag}/meta"] = np.array([active, u], dtype=np.float64)
+    ns = {"layers": layers, "active": 2, "update_factor": 1, "rx_global_model": storage[0],
+          "model_parameters": [a.copy() for a in glob_]}
+    exec(code_lc, ns)
+    for t in range(layers):
+        out[f"learner/out_{t}"] = np.asarray(ns["model_parameters"][t])
+
+    # ---- TF1 CFA_FA server (federated_sample_CNN_CFA_FA.py:73-76 zeros, :86-89, :130-133) and
+    #      client (:280-283), CNN shapes filter 16, number 8, multip 21
+    fa_path = os.path.join(TF1, "federated_sample_CNN_CFA_FA.py")
+    code_zero, span_zero = driver_block(fa_path, "server_w1 = np.zeros", "server_b2 = np.zeros")
+    code_init, span_init = driver_block(fa_path, "server_w1 = server_w1 + balancing_vect[devices] * mathcontent",
+                                        "server_b2 = server_b2 + balancing_vect[devices] * mathcontent")
+    code_round, span_round = driver_block(fa_path, "server_w1 = server_w1 + eps_t_control * balancing_vect[devices] * (mathcontent",
+                                          "server_b2 = server_b2 + eps_t_control * balancing_vect[devices] * (mathcontent")
+    code_cli, span_cli = driver_block(fa_path, "W_val_l1 = W_val_l1 + eps_t_control2", "b_val_l2 = b_val_l2 + eps_t_control2")
+    for k, sp in (("zeros", span_zero), ("init", span_init), ("round", span_round), ("client", span_cli)):
+        out[f"cfa_fa/{k}_src_lines"] = np.array(sp)
+    K = 5
+    shapes = [(16, 1, 8), (8,), (168, 8), (8,)]
+    contents0 = [mat_roundtrip(gen_model(rng, shapes)) for _ in range(K)]
+    contents1 = [mat_roundtrip(gen_model(rng, shapes)) for _ in range(K)]
+    for d in range(K):
+        for key in ("weights1", "biases1", "weights2", "biases2"):
+            out[f"cfa_fa/c0_{key}"] = np.stack([c[key] for c in contents0])
+            out[f"cfa_fa/c1_{key}"] = np.stack([c[key] for c in contents1])
+    ns = {"np": np, "filter": 16, "number": 8, "multip": 21, "balancing_vect": np.ones(K) * (1 / K)}
+    exec(code_zero, ns)
+    for d in range(K):
+        ns["devices"], ns["mathcontent"] = d, contents0[d]
+        exec(code_init, ns)
+    for k, key in enumerate(("server_w1", "server_b1", "server_w2", "server_b2")):
+        out[f"cfa_fa/init_{k}"] = np.asarray(ns[key])
+    ns["eps_t_control"] = 0.7
+    for d in range(K):
+        ns["devices"], ns["mathcontent"] = d, contents1[d]
+        exec(code_round, ns)
+    for k, key in enumerate(("server_w1", "server_b1", "server_w2", "server_b2")):
+        out[f"cfa_fa/round_{k}"] = np.asarray(ns[key])
+    server_file = mat_roundtrip([ns["server_w1"], ns["server_b1"], ns["server_w2"], ns["server_b2"]])
+    W_val = [a for a in gen_model(rng, shapes)]  # the device's fp32 model (TF values)
+    for k, key in enumerate(("weights1", "biases1", "weights2", "biases2")):
+        out[f"cfa_fa/server_file_{key}"] = server_file[key]
+        out[f"cfa_fa/wval_{k}"] = W_val[k]
+    ns2 = {"np": np, "W_val_l1": W_val[0], "b_val_l1": W_val[1], "W_val_l2": W_val[2], "b_val_l2": W_val[3],
+           "eps_t_control2": 0.35, "mathcontent": server_file}
+    exec(code_cli, ns2)
+    for k, key in enumerate(("W_val_l1", "b_val_l1", "W_val_l2", "b_val_l2")):
+        out[f"cfa_fa/client_{k}"] = np.asarray(ns2[key])
+    save("f1_driver_aggregations.npz", **out)
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit(f"reference tree not found at {REF}")
@@ -588,6 +694,7 @@ def main():
     case_tf1_cfa_ge_mobilenet()
     case_tf2()
     case_parameter_server()
+    case_driver_aggregations()
 
 
 if __name__ == "__main__":

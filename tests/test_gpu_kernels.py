@@ -294,6 +294,30 @@ def test_mewma_tf1_f64_identical(gpu, filtered, init, dtypes):
             assert np.array_equal(a, ref_states[k][..., j].astype(np.float64)), (j, k)
 
 
+@pytest.mark.parametrize("rule", [0, 2, 3])
+@pytest.mark.parametrize("n", [0, 1, 4, 17])
+def test_fold_f64_rules(gpu, rule, n):
+    """cfa_fold_f64: SEQUENTIAL / SEQUENTIAL_DIV / ACCUMULATE on fp64 buckets, identical to the
+    numpy fp64 chain (one rounding per operation)."""
+    rng = np.random.default_rng(1400 + 10 * rule + n)
+    P = 20_003
+    local = rng.standard_normal(P)
+    xs = [rng.standard_normal(P) for _ in range(n)]
+    a = [float(v) for v in rng.random(n)]
+    d = [float(v) for v in rng.integers(1, 9, n)]
+    ref = local.copy()
+    for j in range(n):
+        if rule == 0:
+            ref = ref + a[j] * (xs[j] - ref)
+        elif rule == 2:
+            ref = ref + a[j] * (xs[j] - ref) / d[j]
+        else:
+            ref = ref + a[j] * xs[j]
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    gpu.fold_f64(out, _dev64(local), [_dev64(x) for x in xs], a, rule, d if rule == 2 else None)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
 def test_mix_tf1_error_paths(gpu):
     from federated_amd._lib import CFAError
     x = torch.zeros(16, device="cuda")
