@@ -124,3 +124,28 @@ def test_config5_ring_round_world1(gpu):
     assert shard.alphas == [0.5]
     for i in (0, 1, 77, 127):
         assert np.array_equal(out[i], sequential_mix(h[i], [h[(i - 1) % 128]], [0.5]))
+
+
+@pytest.mark.parametrize("P", [24_622, 2_100_003])  # one population launch / per-device streaming mixes
+def test_graph_population_round_world1(gpu, P):
+    """Arbitrary topology (vGraph rows with the random.choices draw) as one shard: the round
+    equals per-device sequential mixes on the oracle, bit for bit."""
+    import random as _random
+    from federated_amd import topology as T
+    from federated_amd.graph_population import GraphPopulationShard, GraphShardPlan
+    rng = np.random.default_rng(9)
+    D = 12
+    g = (rng.random((D, D)) < 0.4).astype(np.uint8)
+    g = np.maximum(g, g.T)
+    np.fill_diagonal(g, 0)
+    lists = T.mobile(g[:, :, None], 0, 3, rng=_random.Random(3))
+    plan = GraphShardPlan(lists, 0, 1)
+    shard = GraphPopulationShard(plan, P, torch.device("cuda"), None, gpu)
+    shard.models.normal_()
+    shard.round()
+    torch.cuda.synchronize()
+    h = shard.models.cpu().numpy()
+    out = shard.mixed.cpu().numpy()
+    for i in range(D):
+        nb = lists[i]
+        assert np.array_equal(out[i], sequential_mix(h[i], [h[j] for j in nb], T.alphas_tf2(nb, i, D))), i
