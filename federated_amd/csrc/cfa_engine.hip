@@ -1472,3 +1472,17 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_trav
   else return fail(CFA_E_INVALID, "unknown traversal mode");
   return check_launch("mix8_trav");
 }
+
+// Experiment (not part of the public header): device allocations with explicit hipExtMalloc
+// flags (0 default, 3 uncached, 4 physically contiguous), for tools/alloc_experiment.py.
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_malloc(void** p, size_t bytes,
+                                                                              unsigned flags) {
+  hipError_t e = hipExtMallocWithFlags(p, bytes, flags);
+  if (e != hipSuccess) return fail(CFA_E_HIP, "hipExtMallocWithFlags(%zu, 0x%x): %s", bytes, flags, hipGetErrorString(e));
+  return CFA_OK;
+}
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_free(void* p) {
+  hipError_t e = hipFree(p);
+  if (e != hipSuccess) return fail(CFA_E_HIP, "hipFree: %s", hipGetErrorString(e));
+  return CFA_OK;
+}
