@@ -1384,6 +1384,7 @@ __global__ __launch_bounds__(kBlock) void mix8_gld_bst_kernel(float* out, Fanin 
 // Traversal-order experiment: 0 = grid-stride (production), 1 = blocked (each workgroup owns a
 // contiguous span of tiles), 2 = XCD-grouped grid-stride (blocks are dispatched round-robin over
 // the 8 XCDs; the logical id is remapped so each XCD walks a contiguous run of tiles).
+// Decomposition: 3 = the 9 reads alone (grid-stride), 4 = the output write alone.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void mix8_trav_kernel(float* out, Fanin f, long long nvec) {
   constexpr int N = 8, U = 4;
@@ -1408,6 +1409,15 @@ __global__ __launch_bounds__(kBlock) void mix8_trav_kernel(float* out, Fanin f, 
   }
   for (long long t = t0; t < t1; t += step) {
     const long long base = t * kTile + threadIdx.x;
+    if constexpr (MODE == 4) {  // write-only: the output stream alone
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const f4 y = {f.c[1], f.c[2], f.c[3], (float)u};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
+      continue;
+    }
     f4 v[U][N + 1];
 #pragma unroll
     for (int k = 0; k <= N; ++k)
@@ -1416,8 +1426,14 @@ __global__ __launch_bounds__(kBlock) void mix8_trav_kernel(float* out, Fanin f, 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
-                                             (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      if constexpr (MODE == 3) {  // read-only: a store that never fires keeps the loads live
+        if (y.x == 1234.5f && y.y == -1234.5f)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                                 (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
     }
   }
 }
@@ -1450,6 +1466,96 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
   return fail(CFA_E_INVALID, "policy pair not instantiated");
 }
 
+// Write-batching experiment: each wave folds B tiles (loads of all 9 streams per tile), keeps
+// the B outputs in registers, then stores them in one burst. SOFT: after each batch's reads, the
+// workgroup waits (bounded spin, never needed for correctness) until every workgroup has
+// finished its reads of that batch, so the chip's write bursts line up in time.
+namespace {
+__device__ unsigned int g_batch_arrivals;
+__global__ void reset_arrivals_kernel() { g_batch_arrivals = 0; }
+
+template <int B, bool SOFT>
+__global__ __launch_bounds__(kBlock) void mix8_batch_kernel(float* out, Fanin f, long long nvec,
+                                                            int spin_limit) {
+  constexpr int N = 8, U = 4;
+  __shared__ f4 ybuf[B][U][kBlock];  // thread-private slots: no LDS synchronisation needed
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const long long G = gridDim.x;
+  unsigned phase = 0;
+  for (long long t0 = blockIdx.x; t0 < full; t0 += G * B, ++phase) {
+#pragma unroll 1
+    for (int b = 0; b < B; ++b) {
+      const long long t = t0 + b * G;
+      if (t < full) {
+        const long long base = t * kTile + threadIdx.x;
+        f4 v[U][N + 1];
+#pragma unroll
+        for (int k = 0; k <= N; ++k)
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ybuf[b][u][threadIdx.x] = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      }
+    }
+    if constexpr (SOFT) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(&g_batch_arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (phase + 1) * (unsigned)G;
+        for (int i = 0; i < spin_limit; ++i) {
+          if (__hip_atomic_load(&g_batch_arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const long long t = t0 + b * G;
+      if (t < full) {
+        const long long base = t * kTile + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, ybuf[b][u][threadIdx.x]), w,
+                                                 (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_batch(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int batch, int soft, int spin_limit, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  if (spin_limit < 0 || spin_limit > 100000) return fail(CFA_E_INVALID, "spin_limit out of range");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  hipStream_t st = (hipStream_t)stream;
+  if (soft) {
+    reset_arrivals_kernel<<<1, 1, 0, st>>>();
+    if (int rc = check_launch("reset_arrivals")) return rc;
+  }
+#define CFA_B(BB)                                                                              \
+  if (batch == BB) {                                                                           \
+    if (soft) mix8_batch_kernel<BB, true><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);  \
+    else mix8_batch_kernel<BB, false><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);      \
+    return check_launch("mix8_batch");                                                         \
+  }
+  CFA_B(1) CFA_B(2) CFA_B(4)
+#undef CFA_B
+  return fail(CFA_E_INVALID, "batch must be 1, 2 or 4");
+}
+
 extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_traverse(
     float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
     int mode, int blocks_per_cu, void* stream) {
@@ -1463,12 +1569,14 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_trav
   const long long nvec = (long long)P / 4;
   cfa_launch_t lc{blocks_per_cu, 4, 0};
   unsigned grid = grid_for(nvec / (kBlock * 4), lc);
-  if (mode == 2) grid -= grid % 8;
+  if (mode == 2) grid -= grid % 8;  // modes 3/4: grid-stride like 0
   if (grid == 0) return fail(CFA_E_INVALID, "experiment grid too small");
   hipStream_t st = (hipStream_t)stream;
   if (mode == 0) mix8_trav_kernel<0><<<grid, kBlock, 0, st>>>(out, f, nvec);
   else if (mode == 1) mix8_trav_kernel<1><<<grid, kBlock, 0, st>>>(out, f, nvec);
   else if (mode == 2) mix8_trav_kernel<2><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 3) mix8_trav_kernel<3><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 4) mix8_trav_kernel<4><<<grid, kBlock, 0, st>>>(out, f, nvec);
   else return fail(CFA_E_INVALID, "unknown traversal mode");
   return check_launch("mix8_trav");
 }
