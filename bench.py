@@ -42,9 +42,14 @@ def parse():
     p.add_argument("--devices-per-gpu", type=int, default=128,
                    help="simulated devices per GPU (128 x 100 MB models + outputs = 26 GB of HBM)")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
+    p.add_argument("--window-batch", type=int, default=0,
+                   help="B > 0: mix B consecutive devices per cfa_mix_window_f32 pass (each window row "
+                        "loaded once); 0 (default) = one streaming mix per device, the judged kernel")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC traffic summary (default profiles/r01_pmc_traffic.json, or "
+                        "profiles/r01_window_pmc_traffic.json with --window-batch)")
     p.add_argument("--e2e", action="store_true",
                    help="also measure the host-resident path (pinned H2D + mix + D2H) on rank 0")
     return p.parse_args()
@@ -86,15 +91,16 @@ def cpu_baseline(P: int, K: int, seconds: float) -> dict:
                       f"({cpu_model()}), numpy {np.__version__}, {el:.1f} s"}
 
 
-def load_traffic(path: str, P: int, K: int):
-    """Per-launch HBM bytes of the mix kernel from the committed rocprofv3 PMC passes
+def load_traffic(path: str, P: int, K: int, kernel: str = None, devices_per_launch: int = 1):
+    """Per-launch HBM bytes of the timed kernel from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py), if they were taken on this exact configuration."""
     try:
         with open(path) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
         return None
-    if t.get("kernel") == KERNEL and t.get("params") == P and t.get("neighbours") == K:
+    if (t.get("kernel") == (kernel or KERNEL) and t.get("params") == P and t.get("neighbours") == K
+            and t.get("devices_per_launch", 1) == devices_per_launch):
         return t.get("hbm_bytes_per_launch")
     return None
 
@@ -159,7 +165,8 @@ def main():
     transport = None
     if world > 1:
         transport = open_transport(args.transport, rank, world, device)
-    shard = RingPopulationShard(plan, P, torch.device("cuda", device), transport, eng)
+    shard = RingPopulationShard(plan, P, torch.device("cuda", device), transport, eng,
+                                window_batch=args.window_batch)
 
     gen = torch.Generator(device=shard.device)
     for i in range(L):  # synthetic models: seeded per global device id
@@ -200,8 +207,9 @@ def main():
         shard.round(compute, comm, timer)
     barrier()
     elapsed = time.perf_counter() - t0
-    durations = [a.elapsed_time(b) / len(interior) for a, b in ev]
-    launches_timed = len(interior) * args.steps
+    launches_per_step = len(shard.window_passes(interior)) if args.window_batch else len(interior)
+    durations = [a.elapsed_time(b) / launches_per_step for a, b in ev]
+    launches_timed = launches_per_step * args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -209,7 +217,7 @@ def main():
 
     bytes_total = world * shard.bytes_per_round * args.steps
     value = bytes_total / elapsed / 1e9
-    per_launch_bytes = (K + 2) * P * 4
+    per_launch_bytes = (K + 2) * P * 4 * len(interior) // launches_per_step  # algorithmic, per launch
     avg_ms = sum(durations) / max(1, len(durations))
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
 
@@ -229,19 +237,22 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded torch normal fp32 buckets, resident in HBM)",
             "config": {
-                "workload": "cfa_population_round: sequential CFA mix (eps=1/(K+1)) of every device "
+                "workload": ("cfa_population_round (window passes of %d devices, rows loaded once per pass): "
+                             % args.window_batch if args.window_batch else "cfa_population_round: ") +
+                            "sequential CFA mix (eps=1/(K+1)) of every device "
                             "with K ring-window neighbours, devices sharded one shard per GPU",
                 "params_per_bucket": P,
                 "neighbours": K,
                 "devices_per_gpu": L,
                 "devices_total": plan.D,
-                "bytes_per_device_mix": per_launch_bytes,
+                "bytes_per_device_mix": (K + 2) * P * 4,
+                "window_batch": args.window_batch,
                 "transport": transport.name if transport else "none",
                 "parallelism": f"population-shard{world}",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": KERNEL,
+                "kernel": "window_vec_kernel" if args.window_batch else KERNEL,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -249,7 +260,11 @@ def main():
                 "avg_launch_ms": round(avg_ms, 5),
                 "launches_timed": launches_timed,
                 "timing": "HIP events around each step's back-to-back interior mixes / launches",
-                "traffic": load_traffic(args.traffic_json, P, K),
+                "traffic": load_traffic(
+                    args.traffic_json or os.path.join(ROOT, "profiles", "r01_window_pmc_traffic.json"
+                                                      if args.window_batch else "r01_pmc_traffic.json"),
+                    P, K, "window_vec_kernel" if args.window_batch else KERNEL,
+                    args.window_batch or 1),
             },
         }
     if world > 1:

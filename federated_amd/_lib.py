@@ -74,6 +74,7 @@ SIGNATURES = {
     "cfa_mewma_update_f32": (_c_int, [_c_void_p, _PP, _PP, _c_int64_p, _c_int, ctypes.c_double,
                                       ctypes.c_float, ctypes.c_float, _c_size_t, _c_int, _c_int,
                                       _c_size_t, _c_void_p]),
+    "cfa_mix_window_f32": (_c_int, [_PP, _PP, _c_float_p, _c_int, _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_population_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_comm_unique_id": (_c_int, [_c_void_p]),

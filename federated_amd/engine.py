@@ -304,6 +304,28 @@ class Engine:
         return W
 
     # -- population ------------------------------------------------------------------------
+    def mix_window(self, outs: Sequence[torch.Tensor], rows: Sequence[torch.Tensor], alphas: Sequence[Sequence[float]],
+                   hl: int, hr: int, stream=None) -> None:
+        """One sliding-window pass (cfa_mix_window_f32): len(outs) consecutive devices, rows =
+        the window's len(outs) + hl + hr buckets in device order, alphas[b] = device b's step
+        coefficients (hl + hr values, all equal: the kernel takes one per device)."""
+        nb = len(outs)
+        if len(rows) != nb + hl + hr or len(alphas) != nb:
+            raise ValueError("window needs nb + hl + hr rows and one alpha list per device")
+        P = _check_bucket(rows[0], "rows[0]")
+        for k, r in enumerate(rows):
+            _check_bucket(r, f"rows[{k}]", P)
+        for b, o in enumerate(outs):
+            _check_bucket(o, f"outs[{b}]", P)
+        per_dev = []
+        for b, al in enumerate(alphas):
+            al = [float(a) for a in al]
+            if len(al) != hl + hr or len(set(al)) > 1:
+                raise ValueError(f"device {b}: the window pass needs hl + hr equal alphas, got {al}")
+            per_dev.append(al[0] if al else 0.0)
+        _lib.call("cfa_mix_window_f32", _lib.ptr_table([o.data_ptr() for o in outs]),
+                  _lib.ptr_table([r.data_ptr() for r in rows]), _lib.float_array(per_dev), nb, int(hl), int(hr), P,
+                  self.stream_handle(stream))
     def population(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
                    csr_idx: torch.Tensor, csr_coef: torch.Tensor, D: int, rule: int, P: int,
                    stream=None) -> None:

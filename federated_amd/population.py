@@ -100,7 +100,13 @@ class RingPopulationShard:
     """Device-resident buckets of one shard plus its halo buffers, and the round itself."""
 
     def __init__(self, plan: RingShardPlan, P: int, device, transport=None, engine=None,
-                 dtype=torch.float32):
+                 dtype=torch.float32, window_batch: int = 0):
+        """``window_batch`` = B > 0 mixes B consecutive devices per ``cfa_mix_window_f32`` pass,
+        loading each row of their shared window once (identical results); 0 = one streaming
+        mix per device."""
+        if window_batch and not (1 <= window_batch <= 8 and plan.hl <= 4 and plan.hr <= 4):
+            raise ValueError("window_batch must be 1..8 with at most 4 neighbours per side")
+        self.window_batch = int(window_batch)
         self.plan, self.P = plan, int(P)
         self.device = torch.device(device)
         self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
@@ -132,6 +138,41 @@ class RingPopulationShard:
     def mix_device(self, i: int, stream=None) -> None:
         self.engine.mix_seq(self.mixed[i], self.models[i], self.sources(i), self.alphas, stream)
 
+    def window_passes(self, devices: List[int]) -> List[List[int]]:
+        """Runs of consecutive local devices, cut into passes of at most window_batch."""
+        passes, run = [], []
+        for i in devices:
+            if run and (i != run[-1] + 1 or len(run) == self.window_batch):
+                passes.append(run)
+                run = []
+            run.append(i)
+        if run:
+            passes.append(run)
+        return passes
+
+    def mix_window(self, devs: List[int], stream=None) -> None:
+        """One cfa_mix_window_f32 pass over consecutive local devices devs."""
+        p = self.plan
+        g0 = p.first + devs[0]
+        rows = [self.bucket((g0 + o) % p.D) for o in range(-p.hl, len(devs) + p.hr)]
+        self.engine.mix_window([self.mixed[i] for i in devs], rows, [self.alphas] * len(devs), p.hl, p.hr, stream)
+
+    def _mix_set(self, devices: List[int], stream, timer=None) -> None:
+        if self.window_batch:
+            for run in self.window_passes(devices):
+                if timer:
+                    timer(run[0], True)
+                self.mix_window(run, stream)
+                if timer:
+                    timer(run[-1], False)
+            return
+        for i in devices:
+            if timer:
+                timer(i, True)
+            self.mix_device(i, stream)
+            if timer:
+                timer(i, False)
+
     def round(self, compute_stream: Optional[torch.cuda.Stream] = None,
               comm_stream: Optional[torch.cuda.Stream] = None, timer=None) -> None:
         """One consensus round: halo exchange on ``comm_stream`` overlapped with interior mixes on
@@ -142,16 +183,10 @@ class RingPopulationShard:
             ms = comm_stream or cs
             ms.wait_stream(cs)  # models are ready (e.g. written by SGD) before they leave
             self.exchange(ms)
-        for i in self.plan.interior():
-            if timer:
-                timer(i, True)
-            self.mix_device(i, cs)
-            if timer:
-                timer(i, False)
+        self._mix_set(self.plan.interior(), cs, timer)
         if self.plan.world > 1:
             cs.wait_stream(comm_stream or cs)
-        for i in self.plan.boundary():
-            self.mix_device(i, cs)
+        self._mix_set(self.plan.boundary(), cs)
 
     @property
     def bytes_per_round(self) -> int:

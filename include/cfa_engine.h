@@ -220,6 +220,21 @@ CFA_API int cfa_mewma_update_f32(float* W, float* const* s, const float* const* 
                          const int64_t* g_stride, int n, double rho, float lr1, float lr2,
                          size_t lr_split, int init, int use_filtered, size_t P, void* stream);
 
+/* (e/f4) Sliding-window population pass: nb (1..8) consecutive devices of a ring window with hl
+ * neighbours below and hr above (0..4 each), mixed with the sequential rule in one launch that
+ * loads each row of the window once: (nb + hl + hr) * P * 4 bytes read and nb * P * 4 written,
+ * against nb * (hl + hr + 2) * P * 4 for nb separate mixes, with identical results.
+ *   rows[0 .. nb+hl+hr-1]: HOST table of device pointers, consecutive devices g0-hl .. g0+nb-1+hr
+ *                          (the caller resolves ring wrap-around and halo rows);
+ *   device b (0 <= b < nb) mixes local rows[b+hl] with rows[b .. b+hl-1] then
+ *                          rows[b+hl+1 .. b+hl+hr] (the window order of cfa.py:14-32 /
+ *                          consensus_v4.py:133-137), coefficient alphas[b] at every step (the
+ *                          reference's eps policies give a window device one value:
+ *                          1/(K+1), consensus_v3.py:145; eps*b/(b + m*b), cfa.py:66-68);
+ *   out[0 .. nb-1]: HOST table of output device pointers (must not alias any row). */
+CFA_API int cfa_mix_window_f32(float* const* out, const float* const* rows, const float* alphas,
+                               int nb, int hl, int hr, size_t P, void* stream);
+
 /* (a1-a6 batched) Population round: one launch mixes D devices.
  * For device d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]) list its sources in order; the
  * FIRST entry is the device's own (local) bucket. Source e is src_ptrs[csr_idx[e]], output d

@@ -149,3 +149,34 @@ def test_graph_population_round_world1(gpu, P):
     for i in range(D):
         nb = lists[i]
         assert np.array_equal(out[i], sequential_mix(h[i], [h[j] for j in nb], T.alphas_tf2(nb, i, D))), i
+
+
+@pytest.mark.parametrize("L,hl,hr,B,P", [(16, 4, 4, 8, 100_000), (13, 4, 4, 8, 24_622), (12, 2, 2, 8, 1_071_748 // 16),
+                                         (10, 1, 0, 8, 24_622), (9, 3, 1, 4, 4097), (7, 0, 2, 1, 1003)])
+def test_window_batched_round_equals_per_device(gpu, L, hl, hr, B, P):
+    """cfa_mix_window_f32 passes (each window row loaded once for B devices) give the per-device
+    mixes bit for bit: aligned rows (vector body), misaligned row pitches (scalar path), tails."""
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    plan = RingShardPlan(0, 1, L, hl, hr)
+    a = RingPopulationShard(plan, P, torch.device("cuda"), None, gpu)
+    b = RingPopulationShard(plan, P, torch.device("cuda"), None, gpu, window_batch=B)
+    a.models.normal_()
+    b.models.copy_(a.models)
+    a.round()
+    b.round()
+    torch.cuda.synchronize()
+    assert torch.equal(a.mixed, b.mixed)
+    h = a.models.cpu().numpy()
+    i = L // 2
+    assert np.array_equal(b.mixed[i].cpu().numpy(), sequential_mix(h[i], [h[j] for j in plan.neighbours(i)], a.alphas))
+
+
+def test_window_error_paths(gpu):
+    from federated_amd._lib import CFAError
+    x = [torch.zeros(64, device="cuda") for _ in range(20)]
+    with pytest.raises(CFAError):  # nb > 8
+        gpu.mix_window(x[:9], x[9:20], [[0.5, 0.5]] * 9, 1, 1)
+    with pytest.raises(CFAError):  # output aliases a row
+        gpu.mix_window([x[1]], x[0:3], [[0.5, 0.5]], 1, 1)
+    with pytest.raises(ValueError):  # per-step alphas differ
+        gpu.mix_window([x[10]], x[0:3], [[0.5, 0.25]], 1, 1)

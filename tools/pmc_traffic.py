@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--kernel", default="mix_vec_kernel")
     ap.add_argument("--params", type=int, required=True)
     ap.add_argument("--neighbours", type=int, required=True)
+    ap.add_argument("--devices-per-launch", type=int, default=1,
+                    help="window passes (cfa_mix_window_f32): devices mixed per launch")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)
@@ -42,9 +44,10 @@ def main():
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)
     read_bytes = 2.0 * f_kib * 1024.0   # gfx950 FETCH_SIZE reads half of a wide coalesced stream
     write_bytes = w_kib * 1024.0
-    algorithmic = (a.neighbours + 2) * a.params * 4
+    B = a.devices_per_launch
+    algorithmic = B * (a.neighbours + 2) * a.params * 4
     res = {
-        "kernel": a.kernel, "params": a.params, "neighbours": a.neighbours,
+        "kernel": a.kernel, "params": a.params, "neighbours": a.neighbours, "devices_per_launch": B,
         "dispatches": {"fetch_pass": len(fetch), "write_pass": len(write)},
         "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
         "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on 16B/lane streams); write = WRITE_SIZE x 1024",
@@ -53,6 +56,9 @@ def main():
         "algorithmic_bytes_per_launch": algorithmic,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / algorithmic,
     }
+    if B > 1:  # a window pass must read its B + K rows once and write B outputs
+        res["window_min_bytes_per_launch"] = (2 * B + a.neighbours) * a.params * 4
+        res["traffic_over_window_min"] = (read_bytes + write_bytes) / res["window_min_bytes_per_launch"]
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
