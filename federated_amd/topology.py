@@ -23,6 +23,7 @@ from .consensus import _tf1, _tf2
 from .engine import Engine
 
 RULE_SEQUENTIAL = 0
+WINDOW_MIN_P = 1 << 21  # auto-select window passes above this bucket size
 
 
 # -- neighbour lists for every device ---------------------------------------------------------
@@ -88,6 +89,29 @@ def csr(lists: Sequence[Sequence[int]], policy: Callable, devices: Optional[int]
             np.asarray(coef, dtype=np.float32))
 
 
+def window_shape(lists: Sequence[Sequence[int]], alphas: Sequence[Sequence[float]], max_side: int = 4):
+    """(hl, hr) when every device d's list is the ring window [d-hl .. d-1, d+1 .. d+hr] (mod D)
+    in that order and its alphas are one value, else None: such populations mix with
+    cfa_mix_window_f32 passes instead of the CSR kernel."""
+    D = len(lists)
+    if D == 0:
+        return None
+    nb0 = [int(j) for j in lists[0]]
+    for cand_hl in range(0, min(len(nb0), max_side) + 1):
+        cand_hr = len(nb0) - cand_hl
+        if cand_hr > max_side or cand_hl + cand_hr >= D:
+            continue
+        ok = True
+        for d in range(D):
+            want = [(d + o) % D for o in list(range(-cand_hl, 0)) + list(range(1, cand_hr + 1))]
+            if [int(j) for j in lists[d]] != want or len(set(float(a) for a in alphas[d])) > 1:
+                ok = False
+                break
+        if ok:
+            return cand_hl, cand_hr
+    return None
+
+
 class PopulationRound:
     """A population of D device buckets resident in HBM, mixed in ONE launch per round."""
 
@@ -102,15 +126,35 @@ class PopulationRound:
         self.src = torch.tensor([models[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
         self.dst = torch.tensor([self.out[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
         self.tables = None
+        self.window = None  # (hl, hr, per-device alphas) when the topology is a ring window
 
-    def set_topology(self, lists, policy) -> None:
-        ptr, idx, coef = csr(lists, policy, self.models.shape[0])
+    def set_topology(self, lists, policy, use_window: Optional[bool] = None) -> None:
+        """CSR tables for the one-launch population kernel. A ring-window topology with one
+        coefficient per device (ring / wrap-around windows under every reference eps policy) can
+        run as cfa_mix_window_f32 passes instead (rows loaded once per 8 devices; same results).
+        ``use_window=None`` picks the passes only for buckets above 2M elements: below that the
+        whole population fits the 256 MB Infinity Cache, the single CSR launch already reuses
+        rows there, and per-pass launch cost dominates (tools/bench_configs.py: C4, C5)."""
+        if use_window is None:
+            use_window = self.models.shape[1] > WINDOW_MIN_P
+        D = self.models.shape[0]
+        ptr, idx, coef = csr(lists, policy, D)
         dev = self.models.device
         self.tables = tuple(torch.from_numpy(a).to(dev) for a in (ptr, idx, coef))
+        alphas = [list(policy(nb, d, D)) for d, nb in enumerate(lists)]
+        shape = window_shape(lists, alphas) if use_window else None
+        self.window = (shape[0], shape[1], alphas) if shape else None
 
     def run(self, stream=None) -> torch.Tensor:
         if self.tables is None:
             raise RuntimeError("set_topology() first")
         D, P = self.models.shape
+        if self.window is not None:
+            hl, hr, alphas = self.window
+            for s in range(0, D, 8):
+                devs = list(range(s, min(s + 8, D)))
+                rows = [self.models[(s + o) % D] for o in range(-hl, len(devs) + hr)]
+                self.engine.mix_window([self.out[d] for d in devs], rows, [alphas[d] for d in devs], hl, hr, stream)
+            return self.out
         self.engine.population(self.dst, self.src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
         return self.out

@@ -180,3 +180,27 @@ def test_window_error_paths(gpu):
         gpu.mix_window([x[1]], x[0:3], [[0.5, 0.5]], 1, 1)
     with pytest.raises(ValueError):  # per-step alphas differ
         gpu.mix_window([x[10]], x[0:3], [[0.5, 0.25]], 1, 1)
+
+
+@pytest.mark.parametrize("D,P,hl,hr", [(32, 1_071_748 // 8, 2, 2), (128, 24_622, 1, 0), (19, 50_001, 4, 4)])
+def test_population_round_window_path_equals_csr(gpu, D, P, hl, hr):
+    """topology.PopulationRound on a ring window runs cfa_mix_window_f32 passes; identical to
+    the CSR one-launch kernel and to the oracle."""
+    from federated_amd import topology as T
+    lists = [[(d + o) % D for o in list(range(-hl, 0)) + list(range(1, hr + 1))] for d in range(D)]
+    models = torch.randn(D, P, device="cuda")
+    win = T.PopulationRound(gpu, models)
+    win.set_topology(lists, T.alphas_tf2, use_window=True)
+    assert win.window is not None and win.window[:2] == (hl, hr)
+    auto = T.PopulationRound(gpu, models)
+    auto.set_topology(lists, T.alphas_tf2)
+    assert (auto.window is not None) == (P > T.WINDOW_MIN_P)
+    csr = T.PopulationRound(gpu, models)
+    csr.set_topology(lists, T.alphas_tf2, use_window=False)
+    win.run()
+    csr.run()
+    torch.cuda.synchronize()
+    assert torch.equal(win.out, csr.out)
+    h = models.cpu().numpy()
+    for d in (0, D // 2, D - 1):
+        assert np.array_equal(win.out[d].cpu().numpy(), sequential_mix(h[d], [h[j] for j in lists[d]], T.alphas_tf2(lists[d], d, D)))

@@ -73,3 +73,20 @@ def test_population_round_matches_per_device_calls(gpu, rule):
         a = [float(np.float32(x)) for x in pol(lists[d], d, D)]
         ref = O.sequential_mix(host[d], [host[j] for j in lists[d]], a)
         assert np.array_equal(out[d].cpu().numpy(), ref), (rule, d)
+
+
+def test_window_shape_detection():
+    from federated_amd import topology as T
+    win = lambda D, hl, hr: [[(d + o) % D for o in list(range(-hl, 0)) + list(range(1, hr + 1))] for d in range(D)]
+    pol = lambda lists, p: [p(nb, d, len(lists)) for d, nb in enumerate(lists)]
+    assert T.window_shape(T.ring_v4(16, 1), pol(T.ring_v4(16, 1), T.alphas_tf2)) == (1, 0)
+    assert T.window_shape(win(32, 2, 2), pol(win(32, 2, 2), T.alphas_tf2)) == (2, 2)
+    assert T.window_shape(win(20, 4, 4), pol(win(20, 4, 4), T.alphas_tf2)) == (4, 4)
+    assert T.window_shape(win(20, 0, 3), pol(win(20, 0, 3), T.alphas_tf2)) == (0, 3)
+    # clamped k-regular windows (edges shift) and wider windows stay on the CSR kernel
+    assert T.window_shape(T.kregular_v3(30, 4), pol(T.kregular_v3(30, 4), T.alphas_tf2)) is None
+    assert T.window_shape(T.kregular_tf1(32, 4), pol(T.kregular_tf1(32, 4), T.alphas_tf2)) is None
+    assert T.window_shape(win(40, 5, 5), pol(win(40, 5, 5), T.alphas_tf2)) is None
+    # step-varying coefficients cannot use the one-alpha-per-device window pass
+    lists = win(16, 1, 1)
+    assert T.window_shape(lists, [[0.5, 0.25]] * 16) is None

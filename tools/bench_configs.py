@@ -82,11 +82,11 @@ def tf1_call(shapes, K, N, module, reps=20, **kw):
             "of_which_mat_loads_ms": round(t_io * 1e3, 3), "numpy_arith_ms": round(t_np * 1e3, 3)}
 
 
-def population(D, P, lists, policy, reps=20):
+def population(D, P, lists, policy, reps=20, use_window=None):
     eng = get_engine(0)
     models = torch.randn(D, P, device="cuda")
     pr = T.PopulationRound(eng, models)
-    pr.set_topology(lists, policy)
+    pr.set_topology(lists, policy, use_window)
     pr.run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -103,7 +103,8 @@ def population(D, P, lists, policy, reps=20):
         for d in range(D):
             O.sequential_mix(host[d], [host[j] for j in lists[d]], policy(lists[d], d, D))
     t_np = med_time(numpy_round, 2)
-    return {"devices": D, "P": P, "round_us": round(t * 1e6, 1), "GBps": round(B / t / 1e9, 1),
+    return {"devices": D, "P": P, "path": "window" if pr.window else "csr", "round_us": round(t * 1e6, 1),
+            "GBps": round(B / t / 1e9, 1),
             "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
 
 
@@ -146,8 +147,10 @@ def main():
                  **population(32, 1_071_748, [[(d + o) % 32 for o in (-2, -1, 1, 2)] for d in range(32)], T.alphas_tf2)})
     rows.append({"config": "C5 radar CNN, 128 devices, ring (v4 N=1), one population launch",
                  **population(128, 24_622, T.ring_v4(128, 1), T.alphas_tf2)})
-    rows.append({"config": "C5 at 25M params/device (scaling shape), 32 devices ring",
+    rows.append({"config": "C5 at 25M params/device (scaling shape), 32 devices ring (auto: window passes)",
                  **population(32, 25_000_000, T.ring_v4(32, 1), T.alphas_tf2, reps=5)})
+    rows.append({"config": "C5 at 25M params/device, 32 devices ring, CSR population kernel",
+                 **population(32, 25_000_000, T.ring_v4(32, 1), T.alphas_tf2, reps=5, use_window=False)})
     for r in rows:
         print(json.dumps(r), flush=True)
 
