@@ -124,6 +124,24 @@ def load() -> ctypes.CDLL:
     return _lib
 
 
+EXP_PATH = os.path.join(LIB_DIR, "libcfa_exp.so")
+_exp = None
+
+
+def load_experiments() -> ctypes.CDLL:
+    """The measurement-only library of tools/ (csrc/cfa_experiments.hip); never used by the
+    product. Its entry points are bound by the tools themselves; errors via cfa_exp_last_error."""
+    global _exp
+    load()  # the HIP runtime torch loaded, as for libcfa
+    with _lock:
+        if _exp is None:
+            if not os.path.isfile(EXP_PATH):
+                raise ImportError(f"{EXP_PATH} not found; build it with `make -C federated_amd/csrc`")
+            _exp = ctypes.CDLL(EXP_PATH, mode=ctypes.RTLD_LOCAL)
+            _exp.cfa_exp_last_error.restype = ctypes.c_char_p
+    return _exp
+
+
 def call(name: str, *args) -> None:
     """Invoke a C-ABI entry point; raise CFAError with the library's message on failure."""
     lib = load()

@@ -19,7 +19,7 @@
 
 #include "cfa_engine.h"
 
-// Defined in cfa_engine.hip: records the thread-local message cfa_last_error() returns.
+// Defined in cfa_mix.hip: records the thread-local message cfa_last_error() returns.
 extern "C" void cfa_internal_set_error(const char* msg);
 
 static int comm_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

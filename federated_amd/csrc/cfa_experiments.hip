@@ -1,0 +1,281 @@
+// cfa_experiments.hip — measurement-only kernels, built into lib/libcfa_exp.so for tools/ (never
+// loaded by the product): cache-policy, traversal-order, read/write decomposition and
+// write-batching variants of the 8-neighbour mix, and allocations with explicit hipExtMalloc
+// flags. Results are recorded under profiles/ (DESIGN.md section 3).
+#include "cfa_internal.h"
+
+extern "C" __attribute__((visibility("default"))) const char* cfa_exp_last_error(void) {
+  return g_last_error.c_str();
+}
+
+// ------------------------------------------------------------------------------------------
+// Experiment (not part of the public header): the N = 8, 4-vector mix through buffer loads /
+// stores with explicit gfx950 cache-policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1), used by
+// tools/tune_cache_policy.py to pick the streaming policy of the production kernel.
+// ------------------------------------------------------------------------------------------
+namespace {
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+template <int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void mix8_buf_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  const unsigned bytes = (unsigned)(nvec * 16);
+  __amdgpu_buffer_rsrc_t r[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc((void*)f.src[k], 0, bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, bytes, 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const int base = (int)((t * kTile + threadIdx.x) * 16);
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u4 x = __builtin_amdgcn_raw_buffer_load_b128(r[k], base + u * kBlock * 16, 0, LAUX);
+        v[u][k] = __builtin_bit_cast(f4, x);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w, base + u * kBlock * 16, 0, SAUX);
+    }
+  }
+}
+// global nt loads (as the production kernel) + buffer store with explicit policy
+template <int SAUX>
+__global__ __launch_bounds__(kBlock) void mix8_gld_bst_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                             (int)((base + (long long)u * kBlock) * 16), 0, SAUX);
+    }
+  }
+}
+// Traversal-order experiment: 0 = grid-stride (production), 1 = blocked (each workgroup owns a
+// contiguous span of tiles), 2 = XCD-grouped grid-stride (blocks are dispatched round-robin over
+// the 8 XCDs; the logical id is remapped so each XCD walks a contiguous run of tiles).
+// Decomposition: 3 = the 9 reads alone (grid-stride), 4 = the output write alone.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void mix8_trav_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8, U = 4;
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const long long G = gridDim.x;
+  long long t0, t1, step;
+  if constexpr (MODE == 1) {
+    t0 = full * blockIdx.x / G;
+    t1 = full * (blockIdx.x + 1) / G;
+    step = 1;
+  } else if constexpr (MODE == 2) {
+    const long long per = G / 8;  // host guarantees G % 8 == 0
+    t0 = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    t1 = full;
+    step = G;
+  } else {
+    t0 = blockIdx.x;
+    t1 = full;
+    step = G;
+  }
+  for (long long t = t0; t < t1; t += step) {
+    const long long base = t * kTile + threadIdx.x;
+    if constexpr (MODE == 4) {  // write-only: the output stream alone
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const f4 y = {f.c[1], f.c[2], f.c[3], (float)u};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
+      continue;
+    }
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      if constexpr (MODE == 3) {  // read-only: a store that never fires keeps the loads live
+        if (y.x == 1234.5f && y.y == -1234.5f)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                                 (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int laux, int saux, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_X(L, S) \
+  if (laux == L && saux == S) { mix8_buf_kernel<L, S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_buf"); }
+  CFA_X(0, 0) CFA_X(2, 2) CFA_X(2, 0) CFA_X(0, 2) CFA_X(1, 2) CFA_X(16, 2) CFA_X(17, 2) CFA_X(3, 2)
+  CFA_X(18, 2) CFA_X(19, 2) CFA_X(2, 16) CFA_X(2, 17) CFA_X(2, 18) CFA_X(2, 19) CFA_X(18, 18) CFA_X(17, 17)
+  CFA_X(16, 16) CFA_X(1, 1)
+#undef CFA_X
+#define CFA_G(S) \
+  if (laux == -2 && saux == S) { mix8_gld_bst_kernel<S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_gld"); }
+  CFA_G(0) CFA_G(2) CFA_G(16) CFA_G(17) CFA_G(18) CFA_G(1)
+#undef CFA_G
+  return fail(CFA_E_INVALID, "policy pair not instantiated");
+}
+
+// Write-batching experiment: each wave folds B tiles (loads of all 9 streams per tile), keeps
+// the B outputs in registers, then stores them in one burst. SOFT: after each batch's reads, the
+// workgroup waits (bounded spin, never needed for correctness) until every workgroup has
+// finished its reads of that batch, so the chip's write bursts line up in time.
+namespace {
+__device__ unsigned int g_batch_arrivals;
+__global__ void reset_arrivals_kernel() { g_batch_arrivals = 0; }
+
+template <int B, bool SOFT>
+__global__ __launch_bounds__(kBlock) void mix8_batch_kernel(float* out, Fanin f, long long nvec,
+                                                            int spin_limit) {
+  constexpr int N = 8, U = 4;
+  __shared__ f4 ybuf[B][U][kBlock];  // thread-private slots: no LDS synchronisation needed
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const long long G = gridDim.x;
+  unsigned phase = 0;
+  for (long long t0 = blockIdx.x; t0 < full; t0 += G * B, ++phase) {
+#pragma unroll 1
+    for (int b = 0; b < B; ++b) {
+      const long long t = t0 + b * G;
+      if (t < full) {
+        const long long base = t * kTile + threadIdx.x;
+        f4 v[U][N + 1];
+#pragma unroll
+        for (int k = 0; k <= N; ++k)
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ybuf[b][u][threadIdx.x] = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      }
+    }
+    if constexpr (SOFT) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(&g_batch_arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (phase + 1) * (unsigned)G;
+        for (int i = 0; i < spin_limit; ++i) {
+          if (__hip_atomic_load(&g_batch_arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const long long t = t0 + b * G;
+      if (t < full) {
+        const long long base = t * kTile + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, ybuf[b][u][threadIdx.x]), w,
+                                                 (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_batch(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int batch, int soft, int spin_limit, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  if (spin_limit < 0 || spin_limit > 100000) return fail(CFA_E_INVALID, "spin_limit out of range");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  hipStream_t st = (hipStream_t)stream;
+  if (soft) {
+    reset_arrivals_kernel<<<1, 1, 0, st>>>();
+    if (int rc = check_launch("reset_arrivals")) return rc;
+  }
+#define CFA_B(BB)                                                                              \
+  if (batch == BB) {                                                                           \
+    if (soft) mix8_batch_kernel<BB, true><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);  \
+    else mix8_batch_kernel<BB, false><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);      \
+    return check_launch("mix8_batch");                                                         \
+  }
+  CFA_B(1) CFA_B(2) CFA_B(4)
+#undef CFA_B
+  return fail(CFA_E_INVALID, "batch must be 1, 2 or 4");
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_traverse(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    int mode, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  if (mode == 2) grid -= grid % 8;  // modes 3/4: grid-stride like 0
+  if (grid == 0) return fail(CFA_E_INVALID, "experiment grid too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == 0) mix8_trav_kernel<0><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 1) mix8_trav_kernel<1><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 2) mix8_trav_kernel<2><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 3) mix8_trav_kernel<3><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else if (mode == 4) mix8_trav_kernel<4><<<grid, kBlock, 0, st>>>(out, f, nvec);
+  else return fail(CFA_E_INVALID, "unknown traversal mode");
+  return check_launch("mix8_trav");
+}
+
+// Experiment (not part of the public header): device allocations with explicit hipExtMalloc
+// flags (0 default, 3 uncached, 4 physically contiguous), for tools/alloc_experiment.py.
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_malloc(void** p, size_t bytes,
+                                                                              unsigned flags) {
+  hipError_t e = hipExtMallocWithFlags(p, bytes, flags);
+  if (e != hipSuccess) return fail(CFA_E_HIP, "hipExtMallocWithFlags(%zu, 0x%x): %s", bytes, flags, hipGetErrorString(e));
+  return CFA_OK;
+}
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_free(void* p) {
+  hipError_t e = hipFree(p);
+  if (e != hipSuccess) return fail(CFA_E_HIP, "hipFree: %s", hipGetErrorString(e));
+  return CFA_OK;
+}
+

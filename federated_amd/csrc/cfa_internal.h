@@ -1,0 +1,259 @@
+// cfa_internal.h — shared internals of libcfa's translation units (not installed, not an ABI).
+//
+// Device helpers for gfx950 (MI355X / CDNA4): the float4 streaming loads and stores, the fold of
+// the sequential / linear / FedAvg rules, the compression epilogue, the launch-shape defaults,
+// and the thread-local error reporting behind cfa_last_error(). Every .hip file of the library
+// is compiled with -ffp-contract=off: CFA_RULE_SEQUENTIAL evaluates t = x - w; t = a * t;
+// w = w + t exactly as fp32 numpy does (three roundings), which makes the TF2 path
+// bit-identical to the reference; CFA_RULE_LINEAR uses explicit fmaf.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "cfa_engine.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// Error reporting: one thread-local message per thread, shared by the library's translation
+// units (C++17 inline variable); no global mutable state is shared between threads.
+// ------------------------------------------------------------------------------------------
+inline thread_local std::string g_last_error;
+
+__attribute__((format(printf, 2, 3))) inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define CFA_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(CFA_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                  __FILE__, __LINE__);                                                   \
+  } while (0)
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CFA_E_HIP, "%s launch failed: %s", what, hipGetErrorString(e));
+  return CFA_OK;
+}
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// Default launch configuration (cfa_launch_t), optionally overridden once from the
+// environment (CFA_BLOCKS_PER_CU, CFA_VEC_PER_LANE, CFA_NONTEMPORAL); immutable after first use.
+// Explicit per-call configurations go through cfa_mix_seq_ex_f32.
+// Defaults from the in-process sweep on MI355X (tools/tune_mix.py, profiles/r01_tune.jsonl):
+// 2 resident workgroups per CU with a grid-stride loop, nontemporal loads and stores, and
+// vec_per_lane = 0 (auto: the widest tile that keeps (n+1)*vec <= 40 float4 in registers).
+static int norm_vec(int v) { return v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0)); }
+static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ? 2 : 1); }
+static cfa_launch_t read_tune() {
+  cfa_launch_t t{2, 0, 1};
+  if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
+  if (const char* s = getenv("CFA_VEC_PER_LANE")) t.vec_per_lane = norm_vec(atoi(s));
+  if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
+  return t;
+}
+static const cfa_launch_t& tune() {
+  static const cfa_launch_t t = read_tune();  // C++11 magic static: thread-safe init
+  return t;
+}
+
+static int device_cus() {  // per-device CU count, cached after the first query
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < 64) {
+    const int c = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+    if (c > 0) return c;
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 256;
+  if (dev >= 0 && dev < 64) __atomic_store_n(&cache[dev], cus, __ATOMIC_RELAXED);
+  return cus;
+}
+
+static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
+  if (tiles <= 0) return 1;
+  long long g = tiles;
+  if (t.blocks_per_cu > 0) {
+    long long cap = (long long)device_cus() * t.blocks_per_cu;
+    if (g > cap) g = cap;
+  }
+  if (g > 0x7fffffffLL) g = 0x7fffffffLL;
+  return (unsigned)g;
+}
+
+// Kernel-argument pack: pointers + coefficients land in SGPRs.
+struct Fanin {
+  const float* src[CFA_MAX_FANIN + 1];  // [0] = local (w0), [1..N] = neighbours
+  float c[CFA_MAX_FANIN + 1];           // SEQ: c[j] = alpha of src[j] (c[0] unused); LIN: coeff
+  float d[CFA_MAX_FANIN + 1];           // SEQ_DIV: d[j] = divisor of step j (d[0] unused)
+};
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float* p, long long i) {
+  const f4* q = reinterpret_cast<const f4*>(p) + i;
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, long long i, f4 v) {
+  f4* q = reinterpret_cast<f4*>(p) + i;
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
+template <int N, int RULE>
+__device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
+  if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+    f4 w = v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      f4 t = v[j] - w;  // numpy: (x - w)
+      t = f.c[j] * t;   //        eps * (...)
+      w = w + t;        //        w + (...)
+    }
+    return w;
+  } else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV) {
+    f4 w = v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      f4 t = v[j] - w;  // numpy: (x - w)
+      t = f.c[j] * t;   //        u * (...)
+      t = t / f.d[j];   //        (...) / C   (IEEE-correct fp32 division)
+      w = w + t;
+    }
+    return w;
+  } else {
+    f4 w = f.c[0] * v[0];
+#pragma unroll
+    for (int j = 1; j <= N; ++j) {
+      w.x = fmaf(f.c[j], v[j].x, w.x);
+      w.y = fmaf(f.c[j], v[j].y, w.y);
+      w.z = fmaf(f.c[j], v[j].z, w.z);
+      w.w = fmaf(f.c[j], v[j].w, w.w);
+    }
+    return w;
+  }
+}
+
+// Compression epilogue on one element (TF1/consensus/cfa_ongraphs.py:225-273), fp32 arrays.
+// numpy 2 (NEP 50) casts the Python-float threshold and replacement to fp32, so the test, the
+// product sign(.)*rep and the DPCM sum ref + sign(.)*rep are all fp32 operations (the reference
+// reaches this with fp32 arrays when a call has no neighbour, :218-223). sign(0) = 0 and
+// sign(NaN) = NaN as numpy. The fp64 variant (compress_one_d) serves the fp64 chains.
+__device__ __forceinline__ double np_sign(double x) {
+  return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : x);
+}
+__device__ __forceinline__ float np_signf(float x) {
+  return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x);
+}
+struct CompressParams {
+  int mode;
+  double thr, rep;
+  long long cbegin, cend;  // element range the epilogue applies to
+  unsigned long long* kept;
+};
+__device__ __forceinline__ float compress_one(float y, float ref, const CompressParams& cp,
+                                              unsigned& kept) {
+  const float thr = (float)cp.thr, rep = (float)cp.rep;
+  if (cp.mode == CFA_COMPRESS_SPARSE || cp.mode == CFA_COMPRESS_SPARSE_HI) {
+    if (fabsf(y) < thr) return np_signf(y) * rep;
+  } else if (cp.mode == CFA_COMPRESS_SPARSE_DPCM || cp.mode == CFA_COMPRESS_SPARSE_DPCM_HI) {
+    const float d = y - ref;
+    if (fabsf(d) < thr) return ref + np_signf(d) * rep;
+  }
+  ++kept;
+  return y;
+}
+
+// Block-wide sum of one counter per lane, then a single 64-bit atomic per block.
+__device__ __forceinline__ void block_add_count(unsigned kept, unsigned long long* dst) {
+  __shared__ unsigned red[kBlock / 64];
+  unsigned v = kept;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; ++i) s += red[i];
+    if (s) atomicAdd(dst, s);
+  }
+}
+
+
+// Streaming-policy store (NT kernels): write-through with sc1, so the once-written output does
+// not leave dirty lines in the XCD's L2 (measured +3% over an nt store on the mix kernel,
+// tools/tune_cache_policy.py). Buffer stores take 32-bit offsets: the host splits a vector body
+// into launches of at most kMaxChunkVec float4 (2 GiB).
+constexpr long long kMaxChunkVec = 1LL << 27;
+constexpr int kStoreSc1 = 16;
+
+// fp64 form of the epilogue for the fp64 chains (TF1 W_up_l2 is fp64 in the reference).
+__device__ __forceinline__ double compress_one_d(double y, double ref, const CompressParams& cp,
+                                                 unsigned& kept) {
+  if (cp.mode == CFA_COMPRESS_SPARSE || cp.mode == CFA_COMPRESS_SPARSE_HI) {
+    if (fabs(y) < cp.thr) return np_sign(y) * cp.rep;
+  } else if (cp.mode == CFA_COMPRESS_SPARSE_DPCM || cp.mode == CFA_COMPRESS_SPARSE_DPCM_HI) {
+    const double d = y - ref;
+    if (fabs(d) < cp.thr) return ref + np_sign(d) * cp.rep;
+  }
+  ++kept;
+  return y;
+}
+
+static inline uintptr_t addr(const void* p) { return reinterpret_cast<uintptr_t>(p); }
+
+static int compress_params(int mode, CompressParams& cp) {
+  cp.mode = mode;
+  switch (mode) {
+    case CFA_COMPRESS_NONE: cp.thr = 0.0; cp.rep = 0.0; break;
+    case CFA_COMPRESS_SPARSE: cp.thr = 0.001; cp.rep = 0.0001; break;
+    case CFA_COMPRESS_SPARSE_DPCM: cp.thr = 1.e-4; cp.rep = 1.e-4; break;
+    case CFA_COMPRESS_SPARSE_DPCM_HI: cp.thr = 1.e-3; cp.rep = 1.e-3; break;
+    case CFA_COMPRESS_SPARSE_HI: cp.thr = 0.01; cp.rep = 0.001; break;
+    default: return fail(CFA_E_INVALID, "unknown compression mode %d", mode);
+  }
+  return CFA_OK;
+}
+
+static int validate_mix(const float* out, const float* local, const float* const* nbrs, int n,
+                        size_t P) {
+  if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
+  if (P == 0) return CFA_OK;
+  if (!out || !local) return fail(CFA_E_INVALID, "null out/local bucket");
+  if (n > 0 && !nbrs) return fail(CFA_E_INVALID, "null neighbour table");
+  for (int j = 0; j < n; ++j) {
+    if (!nbrs[j]) return fail(CFA_E_INVALID, "null neighbour bucket %d", j);
+    if (nbrs[j] == out) return fail(CFA_E_INVALID, "output aliases neighbour %d", j);
+  }
+  return CFA_OK;
+}
+
+static bool needs_ref(int mode) {
+  return mode == CFA_COMPRESS_SPARSE_DPCM || mode == CFA_COMPRESS_SPARSE_DPCM_HI;
+}
+}  // namespace

@@ -1,0 +1,449 @@
+// cfa_mix.hip — the streaming mix kernels (fp32 buckets) and their C-ABI: the sequential CFA rule,
+// the FedAvg divisor form, the linear closed form, strided gradient slices, the fused and
+// standalone compression epilogue.
+//
+// The reference computes the mixing step as numpy AXPY chains over whole tensors, one
+// neighbour at a time, with a file round trip between neighbours:
+//   TF1/consensus/cfa.py:66-76, cfa_ongraphs.py:109-119, cfa_ge_2stage.py:73-83 / 594-621,
+//   TF2 consensus_v3.py:153-155, consensus_v4.py:211-213 / 251-253.
+// Here one launch folds every neighbour of a device in registers: each lane streams 16-byte
+// slices of the local bucket and of all n neighbour buckets from HBM, applies the rule, and
+// writes the result once. The work is HBM-bound (0.2-0.45 flop/byte): no MFMA and no LDS
+// staging; coefficients and bucket pointers live in the kernel arguments (SGPRs); every load of
+// a tile is issued before its first use; the fan-in N is a template parameter so the fold is
+// fully unrolled.
+#include "cfa_internal.h"
+
+extern "C" int cfa_version(void) { return CFA_VERSION; }
+extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }
+// Used by cfa_comm.cpp so every translation unit reports through one thread-local message.
+extern "C" __attribute__((visibility("hidden"))) void cfa_internal_set_error(const char* msg) {
+  g_last_error = msg ? msg : "";
+}
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Vector mix kernel: tiles of kBlock*U float4 per block, grid-stride over tiles; the last
+// partial tile is handled with per-vector guards by the block that owns it.
+// ------------------------------------------------------------------------------------------
+template <int N, int RULE, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, long long nvec) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  // (unused and removed by the compiler when !NT)
+  const __amdgpu_buffer_rsrc_t w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<NT>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f4 y = fold<N, RULE>(v[u], f);
+      if constexpr (NT)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
+                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+      else
+        st4<false>(out, base + (long long)u * kBlock, y);
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+      st4<false>(out, i, fold<N, RULE>(v, f));
+    }
+  }
+}
+
+// Vector mix + fused compression epilogue (count reduction per block).
+template <int N>
+__global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fanin f,
+                                                                   long long nvec,
+                                                                   CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (long long)gridDim.x * kBlock) {
+    f4 v[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+    f4 w = fold<N, CFA_RULE_SEQUENTIAL>(v, f);
+    const long long e0 = i * 4;
+    if (e0 + 3 >= cp.cbegin && e0 < cp.cend) {
+      const f4 r = v[0];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const long long e = e0 + c;
+        if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
+      }
+    }
+    st4<false>(out, i, w);
+  }
+  block_add_count(kept, cp.kept);
+}
+
+// Scalar path: unaligned buckets, the <4-element tail, and strided neighbours.
+struct ScalarFanin {
+  const float* src[CFA_MAX_FANIN + 1];
+  long long stride[CFA_MAX_FANIN + 1];
+  float c[CFA_MAX_FANIN + 1];
+  float d[CFA_MAX_FANIN + 1];
+  int n;
+};
+__global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFanin f, long long P,
+                                                            int rule, int compress,
+                                                            CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    const float w0 = f.src[0][i * f.stride[0]];
+    float w;
+    if (rule == CFA_RULE_SEQUENTIAL || rule == CFA_RULE_SEQUENTIAL_DIV) {
+      w = w0;
+      for (int j = 1; j <= f.n; ++j) {
+        float t = f.src[j][i * f.stride[j]] - w;
+        t = f.c[j] * t;
+        if (rule == CFA_RULE_SEQUENTIAL_DIV) t = t / f.d[j];
+        w = w + t;
+      }
+    } else {
+      w = f.c[0] * w0;
+      for (int j = 1; j <= f.n; ++j) w = fmaf(f.c[j], f.src[j][i * f.stride[j]], w);
+    }
+    if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one(w, w0, cp, kept);
+    out[i] = w;
+  }
+  if (compress) block_add_count(kept, cp.kept);
+}
+
+// Standalone compression epilogue (no mixing): y in place.
+__global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float* ref, long long P,
+                                                          CompressParams cp) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    const float r = ref ? ref[i] : 0.0f;
+    y[i] = compress_one(y[i], r, cp, kept);
+  }
+  block_add_count(kept, cp.kept);
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-side dispatch.
+// ------------------------------------------------------------------------------------------
+template <int RULE, int U, bool NT>
+static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const Fanin& f,
+                         long long nvec) {
+#define CFA_CASE(K) \
+  case K:           \
+    mix_vec_kernel<K, RULE, U, NT><<<grid, kBlock, 0, st>>>(out, f, nvec); \
+    break;
+  switch (n) {
+    CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
+    CFA_CASE(7) CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13)
+    CFA_CASE(14) CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
+template <int RULE>
+static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                             const cfa_launch_t& t);
+
+template <int RULE>
+static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                       const cfa_launch_t& t) {
+  // chunks of at most kMaxChunkVec float4 (32-bit buffer offsets of the streaming store)
+  for (long long done = 0; done < nvec; done += kMaxChunkVec) {
+    const long long m = (nvec - done) < kMaxChunkVec ? (nvec - done) : kMaxChunkVec;
+    Fanin g = f;
+    for (int k = 0; k <= n; ++k) g.src[k] = f.src[k] + done * 4;
+    launch_vec_chunk<RULE>(n, st, out + done * 4, g, m, t);
+  }
+}
+
+template <int RULE>
+static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                             const cfa_launch_t& t) {
+  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : auto_vec(n);
+  const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
+  const unsigned grid = grid_for(tiles, t);
+  if (U == 4) {
+    if (t.nontemporal) launch_vec_u<RULE, 4, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 4, false>(n, grid, st, out, f, nvec);
+  } else if (U == 2) {
+    if (t.nontemporal) launch_vec_u<RULE, 2, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 2, false>(n, grid, st, out, f, nvec);
+  } else {
+    if (t.nontemporal) launch_vec_u<RULE, 1, true>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 1, false>(n, grid, st, out, f, nvec);
+  }
+}
+
+static void launch_vec_compress(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                                const CompressParams& cp) {
+  const unsigned grid = grid_for((nvec + kBlock - 1) / kBlock);
+#define CFA_CASE(K) \
+  case K:           \
+    mix_vec_compress_kernel<K><<<grid, kBlock, 0, st>>>(out, f, nvec, cp); \
+    break;
+  switch (n) {
+    CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
+    CFA_CASE(7) CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13)
+    CFA_CASE(14) CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
+// One pass of at most CFA_MAX_FANIN neighbours. Splits the bucket into a scalar head (until
+// every pointer is 16-byte aligned, when they share the same misalignment), a float4 body and
+// a scalar tail. Buckets with different misalignments run entirely on the scalar path.
+static int mix_pass(float* out, const float* local, const float* const* nbrs, const float* c,
+                    int n, size_t P, int rule, const CompressParams* cp, hipStream_t st,
+                    const cfa_launch_t& lc = tune(), const float* div = nullptr) {
+  const uintptr_t mis = addr(out) & 15;
+  bool same = (addr(local) & 15) == mis;
+  for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
+  const bool scalar_only = !same || (mis & 3) != 0;
+  size_t head = 0, nvec = 0;
+  if (!scalar_only) {
+    head = mis ? (16 - mis) / 4 : 0;
+    if (head > P) head = P;
+    nvec = (P - head) / 4;
+  } else {
+    head = P;
+  }
+  const size_t tail_begin = head + nvec * 4;
+
+  CompressParams cpv{};
+  if (cp) cpv = *cp;
+
+  if (nvec > 0) {
+    Fanin f{};
+    f.src[0] = local + head;
+    for (int j = 0; j < n; ++j) f.src[j + 1] = nbrs[j] + head;
+    for (int k = 0; k <= n; ++k) f.c[k] = c[k];
+    for (int k = 0; k <= n; ++k) f.d[k] = div ? div[k] : 1.0f;
+    if (cp) {
+      CompressParams shifted = cpv;
+      shifted.cbegin = cpv.cbegin - (long long)head;
+      shifted.cend = cpv.cend - (long long)head;
+      launch_vec_compress(n, st, out + head, f, (long long)nvec, shifted);
+    } else if (rule == CFA_RULE_SEQUENTIAL) {
+      launch_vec<CFA_RULE_SEQUENTIAL>(n, st, out + head, f, (long long)nvec, lc);
+    } else if (rule == CFA_RULE_SEQUENTIAL_DIV) {
+      launch_vec<CFA_RULE_SEQUENTIAL_DIV>(n, st, out + head, f, (long long)nvec, lc);
+    } else {
+      launch_vec<CFA_RULE_LINEAR>(n, st, out + head, f, (long long)nvec, lc);
+    }
+    if (int rc = check_launch("mix_vec")) return rc;
+  }
+  // Scalar pieces: [0, head) and [tail_begin, P).
+  const size_t pieces[2][2] = {{0, head}, {tail_begin, P}};
+  for (auto& pc : pieces) {
+    const size_t b = pc[0], e = pc[1];
+    if (e <= b) continue;
+    ScalarFanin sf{};
+    sf.src[0] = local + b;
+    sf.stride[0] = 1;
+    for (int j = 0; j < n; ++j) {
+      sf.src[j + 1] = nbrs[j] + b;
+      sf.stride[j + 1] = 1;
+    }
+    for (int k = 0; k <= n; ++k) sf.c[k] = c[k];
+    for (int k = 0; k <= n; ++k) sf.d[k] = div ? div[k] : 1.0f;
+    sf.n = n;
+    CompressParams sc = cpv;
+    sc.cbegin = cpv.cbegin - (long long)b;
+    sc.cend = cpv.cend - (long long)b;
+    const long long len = (long long)(e - b);
+    mix_scalar_kernel<<<grid_for((len + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        out + b, sf, len, rule, cp ? 1 : 0, sc);
+    if (int rc = check_launch("mix_scalar")) return rc;
+  }
+  return CFA_OK;
+}
+
+// Sequential rule over any fan-in: chunks of CFA_MAX_FANIN; chunk k>0 continues from `out`.
+// The compression epilogue is fused into the (single) pass when n <= CFA_MAX_FANIN; wider
+// fan-ins run it as a separate pass with the untouched pre-mix `local` as DPCM reference.
+static int mix_seq_any(float* out, const float* local, const float* const* nbrs,
+                       const float* alphas, int n, size_t P, const CompressParams* cp,
+                       hipStream_t st, const cfa_launch_t& lc = tune()) {
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  const bool split_epilogue = cp && n > CFA_MAX_FANIN;
+  if (split_epilogue && out == local && needs_ref(cp->mode))
+    return fail(CFA_E_INVALID, "in-place DPCM compression needs fan-in <= %d", CFA_MAX_FANIN);
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = 1.0f;
+    for (int j = 0; j < m; ++j) c[j + 1] = alphas[done + j];
+    const CompressParams* fused = (cp && !split_epilogue) ? cp : nullptr;
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL, fused, st, lc))
+      return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  if (split_epilogue)
+    return cfa_compress_epilogue_f32(out + cp->cbegin, local + cp->cbegin, cp->mode,
+                                     (size_t)(cp->cend - cp->cbegin), cp->kept, st);
+  return CFA_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------
+extern "C" int cfa_mix_seq_f32(float* out, const float* local, const float* const* nbrs,
+                               const float* alphas, int n, size_t P, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int cfa_mix_seq_ex_f32(float* out, const float* local, const float* const* nbrs,
+                                  const float* alphas, int n, size_t P,
+                                  const cfa_launch_t* launch, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  cfa_launch_t lc = launch ? *launch : tune();
+  if (lc.blocks_per_cu < 0) return fail(CFA_E_INVALID, "blocks_per_cu < 0");
+  lc.vec_per_lane = norm_vec(lc.vec_per_lane);
+  return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream, lc);
+}
+
+extern "C" int cfa_mix_seq_div_f32(float* out, const float* local, const float* const* nbrs,
+                                   const float* alphas, const float* divisors, int n, size_t P,
+                                   void* stream) {
+  if (n > 0 && (!alphas || !divisors)) return fail(CFA_E_INVALID, "null alphas/divisors");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1], d[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = 1.0f;
+    d[0] = 1.0f;
+    for (int j = 0; j < m; ++j) {
+      c[j + 1] = alphas[done + j];
+      d[j + 1] = divisors[done + j];
+    }
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_SEQUENTIAL_DIV, nullptr, st,
+                          tune(), d))
+      return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,
+                           const float* coeff, int n, size_t P, void* stream) {
+  if (!coeff) return fail(CFA_E_INVALID, "null coefficients");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  float c[CFA_MAX_FANIN + 1];
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    c[0] = done == 0 ? coeff[0] : 1.0f;
+    for (int j = 0; j < m; ++j) c[j + 1] = coeff[done + j + 1];
+    if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_LINEAR, nullptr, st)) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_strided_f32(float* out, const float* local, const float* const* nbrs,
+                                   const int64_t* nbr_stride, const float* alphas, int n, size_t P,
+                                   void* stream) {
+  if (n > 0 && (!alphas || !nbr_stride)) return fail(CFA_E_INVALID, "null alphas/strides");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (P == 0) return CFA_OK;
+  bool unit = true;
+  for (int j = 0; j < n; ++j) {
+    if (nbr_stride[j] < 1) return fail(CFA_E_INVALID, "stride %lld < 1", (long long)nbr_stride[j]);
+    unit = unit && nbr_stride[j] == 1;
+  }
+  if (unit) return cfa_mix_seq_f32(out, local, nbrs, alphas, n, P, stream);
+  hipStream_t st = (hipStream_t)stream;
+  int done = 0;
+  const float* w = local;
+  do {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    ScalarFanin sf{};
+    sf.src[0] = w;
+    sf.stride[0] = 1;
+    sf.c[0] = 1.0f;
+    for (int j = 0; j < m; ++j) {
+      sf.src[j + 1] = nbrs[done + j];
+      sf.stride[j + 1] = nbr_stride[done + j];
+      sf.c[j + 1] = alphas[done + j];
+    }
+    sf.n = m;
+    CompressParams none{};
+    mix_scalar_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        out, sf, (long long)P, CFA_RULE_SEQUENTIAL, 0, none);
+    if (int rc = check_launch("mix_strided")) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_seq_compress_f32(float* out, const float* local, const float* const* nbrs,
+                                        const float* alphas, int n, size_t P, int mode,
+                                        size_t cbegin, size_t cend,
+                                        unsigned long long* kept_count, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  if (!kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  cp.cbegin = (long long)cbegin;
+  cp.cend = (long long)cend;
+  cp.kept = kept_count;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    // No neighbours: out = local, then the epilogue (TF1/consensus/cfa_ongraphs.py:218-223).
+    if (out != local && P > 0)
+      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin,
+                                     kept_count, stream);
+  }
+  return mix_seq_any(out, local, nbrs, alphas, n, P, &cp, st);
+}
+
+extern "C" int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, size_t P,
+                                         unsigned long long* kept_count, void* stream) {
+  if (!kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  if ((mode == CFA_COMPRESS_SPARSE_DPCM || mode == CFA_COMPRESS_SPARSE_DPCM_HI) && !ref && P)
+    return fail(CFA_E_INVALID, "DPCM compression needs a reference bucket");
+  if (P == 0) return CFA_OK;
+  if (!y) return fail(CFA_E_INVALID, "null bucket");
+  cp.cbegin = 0;
+  cp.cend = (long long)P;
+  cp.kept = kept_count;
+  hipStream_t st = (hipStream_t)stream;
+  compress_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+      y, ref, (long long)P, cp);
+  return check_launch("compress");
+}
+

@@ -1,0 +1,308 @@
+// cfa_population.hip — whole-population rounds: the CSR one-launch kernel
+// (cfa_mix_population_f32) and the sliding-window passes (cfa_mix_window_f32) that load each
+// row of a ring window once for up to 8 consecutive devices.
+#include "cfa_internal.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Population round: grid.y = device, grid.x = tiles. CSR lists each device's sources.
+// ------------------------------------------------------------------------------------------
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void population_kernel(float* const* out_ptrs,
+                                                            const float* const* src_ptrs,
+                                                            const int32_t* csr_ptr,
+                                                            const int32_t* csr_idx,
+                                                            const float* csr_coef,
+                                                            long long nvec) {
+  const int d = blockIdx.y;
+  const int e0 = csr_ptr[d];
+  const int e1 = csr_ptr[d + 1];
+  float* out = out_ptrs[d];
+  constexpr int U = 2;
+  constexpr long long kTile = (long long)kBlock * U;
+  for (long long t = blockIdx.x; t * kTile < nvec; t += gridDim.x) {
+    long long idx[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      idx[u] = t * kTile + (long long)u * kBlock + threadIdx.x;
+      ok[u] = idx[u] < nvec;
+    }
+    f4 w[U];
+    const float* s0 = src_ptrs[csr_idx[e0]];
+    const float c0 = csr_coef[e0];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      w[u] = ok[u] ? ld4<true>(s0, idx[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (RULE == CFA_RULE_LINEAR) w[u] = c0 * w[u];
+    }
+    for (int e = e0 + 1; e < e1; ++e) {
+      const float* s = src_ptrs[csr_idx[e]];
+      const float c = csr_coef[e];
+      f4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ok[u] ? ld4<true>(s, idx[u]) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+          f4 tt = x[u] - w[u];
+          tt = c * tt;
+          w[u] = w[u] + tt;
+        } else {
+          w[u].x = fmaf(c, x[u].x, w[u].x);
+          w[u].y = fmaf(c, x[u].y, w[u].y);
+          w[u].z = fmaf(c, x[u].z, w[u].z);
+          w[u].w = fmaf(c, x[u].w, w[u].w);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (ok[u]) st4<true>(out, idx[u], w[u]);
+  }
+}
+
+// Scalar tail for the population kernel (elements [begin, P)).
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void population_tail_kernel(
+    float* const* out_ptrs, const float* const* src_ptrs, const int32_t* csr_ptr,
+    const int32_t* csr_idx, const float* csr_coef, long long begin, long long P) {
+  const int d = blockIdx.y;
+  const long long i = begin + threadIdx.x;
+  if (i >= P) return;
+  const int e0 = csr_ptr[d], e1 = csr_ptr[d + 1];
+  float w = src_ptrs[csr_idx[e0]][i];
+  if constexpr (RULE == CFA_RULE_LINEAR) w = csr_coef[e0] * w;
+  for (int e = e0 + 1; e < e1; ++e) {
+    const float x = src_ptrs[csr_idx[e]][i];
+    const float c = csr_coef[e];
+    if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+      float tt = x - w;
+      tt = c * tt;
+      w = w + tt;
+    } else {
+      w = fmaf(c, x, w);
+    }
+  }
+  out_ptrs[d][i] = w;
+}
+
+// ------------------------------------------------------------------------------------------
+// Sliding-window population pass (cfa_mix_window_f32): nb <= 8 consecutive devices of a ring
+// window (hl below, hr above) share their rows, so each row of the window is loaded ONCE per
+// element for all nb devices: (nb + hl + hr) reads + nb writes instead of nb * (hl + hr + 2).
+// Device b's local row is rows[b + hl]; its neighbours, in the reference window's order
+// (g-hl .. g-1, g+1 .. g+hr), are rows[b .. b+hl-1], rows[b+hl+1 .. b+hl+hr].
+// ------------------------------------------------------------------------------------------
+constexpr int kWinMaxDev = 8;
+struct WindowArgs {
+  const float* rows[kWinMaxDev + 8];
+  float* out[kWinMaxDev];
+  float a[kWinMaxDev];  // one coefficient per device, used for each of its steps
+  int nb;
+};
+
+template <int HL, int HR>
+__device__ __forceinline__ f4 window_fold(const f4* r, int b, const WindowArgs& w) {
+  f4 acc = r[b + HL];
+#pragma unroll
+  for (int j = 0; j < HL; ++j) {
+    f4 t = r[b + j] - acc;
+    t = w.a[b] * t;
+    acc = acc + t;
+  }
+#pragma unroll
+  for (int j = 0; j < HR; ++j) {
+    f4 t = r[b + HL + 1 + j] - acc;
+    t = w.a[b] * t;
+    acc = acc + t;
+  }
+  return acc;
+}
+
+template <int HL, int HR, int U, bool SC1>
+__global__ __launch_bounds__(kBlock) void window_vec_kernel(WindowArgs w, long long nvec) {
+  constexpr int R = kWinMaxDev + HL + HR;
+  constexpr long long kTile = (long long)kBlock * U;
+  const int nr = w.nb + HL + HR;
+  for (long long t = blockIdx.x; t * kTile < nvec; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 r[U][R];
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      if (k < nr)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long i = base + (long long)u * kBlock;
+          if (i < nvec) r[u][k] = ld4<true>(w.rows[k], i);
+        }
+#pragma unroll
+    for (int b = 0; b < kWinMaxDev; ++b)
+      if (b < w.nb) {
+        // (unused and removed by the compiler when !SC1) write-through streaming store
+        const __amdgpu_buffer_rsrc_t o =
+            __builtin_amdgcn_make_buffer_rsrc((void*)w.out[b], 0, (unsigned)(nvec * 16), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long i = base + (long long)u * kBlock;
+          if (i < nvec) {
+            const f4 y = window_fold<HL, HR>(r[u], b, w);
+            if constexpr (SC1)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), o, (int)(i * 16), 0, kStoreSc1);
+            else
+              st4<true>(w.out[b], i, y);
+          }
+        }
+      }
+  }
+}
+
+// Scalar window pass (misaligned rows, the < 4-element tail): runtime hl / hr.
+__global__ __launch_bounds__(kBlock) void window_scalar_kernel(WindowArgs w, int hl, int hr,
+                                                               long long begin, long long P) {
+  for (long long i = begin + (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    for (int b = 0; b < w.nb; ++b) {
+      float acc = w.rows[b + hl][i];
+      for (int j = 0; j < hl; ++j) {
+        float t = w.rows[b + j][i] - acc;
+        t = w.a[b] * t;
+        acc = acc + t;
+      }
+      for (int j = 0; j < hr; ++j) {
+        float t = w.rows[b + hl + 1 + j][i] - acc;
+        t = w.a[b] * t;
+        acc = acc + t;
+      }
+      w.out[b][i] = acc;
+    }
+  }
+}
+
+}  // namespace
+
+namespace {
+struct WindowTune {
+  int vec, sc1, blocks_per_cu;
+};
+static WindowTune window_tune() {  // env overrides for tools/tune_window.py; results identical
+  WindowTune t{1, 0, 6};  // tools/tune_window.py, profiles/r01_tune_window.jsonl
+  if (const char* e = getenv("CFA_WINDOW_VEC")) t.vec = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("CFA_WINDOW_SC1")) t.sc1 = atoi(e) ? 1 : 0;
+  if (const char* e = getenv("CFA_WINDOW_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(e) > 0 ? atoi(e) : 2;
+  return t;
+}
+template <int HL, int HR>
+void launch_window(const WindowArgs& w, long long nvec, hipStream_t st) {
+  const WindowTune t = window_tune();
+  const cfa_launch_t lc{t.blocks_per_cu, t.vec, 1};
+  // chunks of at most kMaxChunkVec float4: 32-bit buffer offsets of the streaming store
+  for (long long done = 0; done < nvec; done += kMaxChunkVec) {
+    const long long m = (nvec - done) < kMaxChunkVec ? (nvec - done) : kMaxChunkVec;
+    WindowArgs c = w;
+    for (int k = 0; k < w.nb + HL + HR; ++k) c.rows[k] = w.rows[k] + done * 4;
+    for (int b = 0; b < w.nb; ++b) c.out[b] = w.out[b] + done * 4;
+    const long long tiles = (m + (long long)kBlock * t.vec - 1) / ((long long)kBlock * t.vec);
+    const unsigned grid = grid_for(tiles, lc);
+    if (t.vec == 1) {
+      if (t.sc1) window_vec_kernel<HL, HR, 1, true><<<grid, kBlock, 0, st>>>(c, m);
+      else window_vec_kernel<HL, HR, 1, false><<<grid, kBlock, 0, st>>>(c, m);
+    } else {
+      if (t.sc1) window_vec_kernel<HL, HR, 2, true><<<grid, kBlock, 0, st>>>(c, m);
+      else window_vec_kernel<HL, HR, 2, false><<<grid, kBlock, 0, st>>>(c, m);
+    }
+  }
+}
+using WindowLaunch = void (*)(const WindowArgs&, long long, hipStream_t);
+#define CFA_W(L, R) &launch_window<L, R>
+const WindowLaunch kWindowLaunch[5][5] = {
+    {CFA_W(0, 0), CFA_W(0, 1), CFA_W(0, 2), CFA_W(0, 3), CFA_W(0, 4)},
+    {CFA_W(1, 0), CFA_W(1, 1), CFA_W(1, 2), CFA_W(1, 3), CFA_W(1, 4)},
+    {CFA_W(2, 0), CFA_W(2, 1), CFA_W(2, 2), CFA_W(2, 3), CFA_W(2, 4)},
+    {CFA_W(3, 0), CFA_W(3, 1), CFA_W(3, 2), CFA_W(3, 3), CFA_W(3, 4)},
+    {CFA_W(4, 0), CFA_W(4, 1), CFA_W(4, 2), CFA_W(4, 3), CFA_W(4, 4)}};
+#undef CFA_W
+}  // namespace
+
+extern "C" int cfa_mix_window_f32(float* const* out, const float* const* rows, const float* alphas,
+                                  int nb, int hl, int hr, size_t P, void* stream) {
+  if (nb < 1 || nb > kWinMaxDev) return fail(CFA_E_INVALID, "nb %d outside 1..%d", nb, kWinMaxDev);
+  if (hl < 0 || hr < 0 || hl > 4 || hr > 4) return fail(CFA_E_INVALID, "window %d/%d outside 0..4", hl, hr);
+  if (!out || !rows || !alphas) return fail(CFA_E_INVALID, "null table");
+  if (P == 0) return CFA_OK;
+  WindowArgs w{};
+  w.nb = nb;
+  const int nr = nb + hl + hr;
+  bool aligned = true;
+  for (int k = 0; k < nr; ++k) {
+    if (!rows[k]) return fail(CFA_E_INVALID, "null row %d", k);
+    w.rows[k] = rows[k];
+    aligned = aligned && (addr(rows[k]) & 15) == 0;
+  }
+  for (int b = 0; b < nb; ++b) {
+    if (!out[b]) return fail(CFA_E_INVALID, "null output %d", b);
+    for (int k = 0; k < nr; ++k)
+      if (out[b] == rows[k]) return fail(CFA_E_INVALID, "output %d aliases row %d", b, k);
+    w.out[b] = out[b];
+    aligned = aligned && (addr(out[b]) & 15) == 0;
+    w.a[b] = alphas[b];
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const long long nvec = aligned ? (long long)(P / 4) : 0;
+  if (nvec > 0) {
+    kWindowLaunch[hl][hr](w, nvec, st);
+    if (int rc = check_launch("window_vec")) return rc;
+  }
+  const long long begin = nvec * 4;
+  if (begin < (long long)P) {
+    const long long len = (long long)P - begin;
+    window_scalar_kernel<<<grid_for((len + kBlock - 1) / kBlock), kBlock, 0, st>>>(w, hl, hr, begin, (long long)P);
+    if (int rc = check_launch("window_scalar")) return rc;
+  }
+  return CFA_OK;
+}
+
+extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                      const int32_t* csr_ptr, const int32_t* csr_idx,
+                                      const float* csr_coef, int D, int rule, size_t P,
+                                      void* stream) {
+  if (D < 0) return fail(CFA_E_INVALID, "negative device count");
+  if (rule != CFA_RULE_SEQUENTIAL && rule != CFA_RULE_LINEAR)
+    return fail(CFA_E_INVALID, "unknown rule %d", rule);
+  if (D == 0 || P == 0) return CFA_OK;
+  if (!out_ptrs || !src_ptrs || !csr_ptr || !csr_idx || !csr_coef)
+    return fail(CFA_E_INVALID, "null population table");
+  if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
+  hipStream_t st = (hipStream_t)stream;
+  // Buckets in a population are expected 16-byte aligned (allocator contract, checked by the
+  // host layer); the body runs on float4, the <4-element tail on the scalar kernel.
+  const long long nvec = (long long)P / 4;
+  if (nvec > 0) {
+    const long long tiles = (nvec + 2LL * kBlock - 1) / (2LL * kBlock);
+    long long gx = tiles;
+    const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+    if (gx > cap) gx = cap < 1 ? 1 : cap;
+    dim3 grid((unsigned)gx, (unsigned)D);
+    if (rule == CFA_RULE_SEQUENTIAL)
+      population_kernel<CFA_RULE_SEQUENTIAL><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                      csr_idx, csr_coef, nvec);
+    else
+      population_kernel<CFA_RULE_LINEAR><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                  csr_idx, csr_coef, nvec);
+    if (int rc = check_launch("population")) return rc;
+  }
+  const long long begin = nvec * 4;
+  if (begin < (long long)P) {
+    dim3 grid(1, (unsigned)D);
+    if (rule == CFA_RULE_SEQUENTIAL)
+      population_tail_kernel<CFA_RULE_SEQUENTIAL><<<grid, 64, 0, st>>>(
+          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
+    else
+      population_tail_kernel<CFA_RULE_LINEAR><<<grid, 64, 0, st>>>(
+          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
+    if (int rc = check_launch("population_tail")) return rc;
+  }
+  return CFA_OK;
+}
+

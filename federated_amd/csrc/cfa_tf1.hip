@@ -1,0 +1,411 @@
+// cfa_tf1.hip — the reference's TF1 numerics under numpy 2 (fp32 first subtraction, fp64 after),
+// on fp32 buckets rounded once (cfa_mix_tf1_f32) or on fp64 buckets unrounded (cfa_mix_tf1_f64,
+// cfa_fold_f64, cfa_mewma_tf1_f64): TF1/consensus/cfa.py:69-76, cfa_ongraphs.py:112-119 and
+// 225-273, cfa_ge_2stage.py:76-83, 331-371, 593-621; the fp64 server-side folds of
+// FL_over_MQTT/PS_server.py:130-133, learner_consensus.py:151-152,
+// federated_sample_CNN_CFA_FA.py:86-89, 130-133, 280-283.
+#include "cfa_internal.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// TF1 numerics (cfa_mix_tf1_f32): the reference's chain under numpy 2 is fp32 for the first
+// subtraction and fp64 after it (eps * wf is an np.float64), so w is carried in double and
+// rounded to fp32 once, after the (fp64) compression epilogue. Fan-ins above CFA_MAX_FANIN
+// chain passes through an fp64 scratch bucket (FROM64 / TO64).
+// ------------------------------------------------------------------------------------------
+struct Tf1Fanin {
+  const float* local;               // pre-mix local: step-0 input and DPCM reference
+  const double* w64;                // running fp64 w of the previous pass (FROM64)
+  const float* src[CFA_MAX_FANIN];  // neighbours of this pass
+  double a[CFA_MAX_FANIN];          // eps * wf_j
+};
+
+template <int N, bool FROM64, bool TO64>
+__global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin f, long long nvec,
+                                                              CompressParams cp, int compress) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (long long)gridDim.x * kBlock) {
+    f4 x[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = ld4<true>(f.src[k], i);
+    const f4 l = ld4<true>(f.local, i);
+    double w[4];
+    constexpr int j0 = FROM64 ? 0 : 1;
+    if constexpr (FROM64) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w[c] = f.w64[4 * i + c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float d = x[0][c] - l[c];         // fp32 - fp32 (both operands fp32)
+        w[c] = (double)l[c] + f.a[0] * (double)d;  // np.float64 * fp32 -> fp64; fp32 + fp64 -> fp64
+      }
+    }
+#pragma unroll
+    for (int j = j0; j < N; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
+    if constexpr (TO64) {
+      double* o = reinterpret_cast<double*>(out) + 4 * i;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[c] = w[c];
+    } else {
+      if (compress) {
+        const long long e0 = i * 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
+      }
+      const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+      st4<true>(reinterpret_cast<float*>(out), i, y);
+    }
+  }
+  if (!TO64 && compress) block_add_count(kept, cp.kept);
+}
+
+// Scalar TF1 path (misaligned buckets, head and tail pieces).
+__global__ __launch_bounds__(kBlock) void mix_tf1_scalar_kernel(void* out, int to64, Tf1Fanin f,
+                                                                int n, long long P,
+                                                                CompressParams cp, int compress) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    const float l = f.local[i];
+    double w;
+    int j = 0;
+    if (f.w64) {
+      w = f.w64[i];
+    } else {
+      const float d = f.src[0][i] - l;
+      w = (double)l + f.a[0] * (double)d;
+      j = 1;
+    }
+    for (; j < n; ++j) w = w + f.a[j] * ((double)f.src[j][i] - w);
+    if (to64) {
+      reinterpret_cast<double*>(out)[i] = w;
+    } else {
+      if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one_d(w, l, cp, kept);
+      reinterpret_cast<float*>(out)[i] = (float)w;
+    }
+  }
+  if (!to64 && compress) block_add_count(kept, cp.kept);
+}
+
+// fp64 buckets (cfa_mix_tf1_f64 / cfa_mewma_tf1_f64): the reference's TF1 arrays as they are
+// (fp32 values widened exactly, fp64 values untouched), the same fp64 operations, no rounding.
+struct F64Fanin {
+  const double* src[CFA_MAX_FANIN + 1];  // [0] = running w (local or previous pass), [1..m]
+  double a[CFA_MAX_FANIN + 1];
+  double d[CFA_MAX_FANIN + 1];           // SEQUENTIAL_DIV divisors
+  int m;
+};
+// rule: CFA_RULE_SEQUENTIAL  w = w + a*(x - w)
+//       CFA_RULE_SEQUENTIAL_DIV  w = w + (a*(x - w))/d
+//       CFA_RULE_ACCUMULATE  w = w + a*x
+__global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fanin f, long long P,
+                                                             int rule, int step0_f32,
+                                                             const double* ref, CompressParams cp,
+                                                             int compress) {
+  unsigned kept = 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    double w = f.src[0][i];
+    int j = 1;
+    if (step0_f32 && f.m >= 1) {  // both operands fp32 arrays in the reference: fp32 subtraction
+      const float d = (float)f.src[1][i] - (float)w;
+      w = w + f.a[1] * (double)d;
+      j = 2;
+    }
+    if (rule == CFA_RULE_SEQUENTIAL) {
+      for (; j <= f.m; ++j) w = w + f.a[j] * (f.src[j][i] - w);
+    } else if (rule == CFA_RULE_SEQUENTIAL_DIV) {
+      for (; j <= f.m; ++j) w = w + (f.a[j] * (f.src[j][i] - w)) / f.d[j];
+    } else {
+      for (; j <= f.m; ++j) w = w + f.a[j] * f.src[j][i];
+    }
+    if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one_d(w, ref[i], cp, kept);
+    out[i] = w;
+  }
+  if (compress) block_add_count(kept, cp.kept);
+}
+
+struct MewmaF64Args {
+  double* W;
+  double* s[CFA_MAX_FANIN];
+  const double* g[CFA_MAX_FANIN];
+  long long gstride[CFA_MAX_FANIN];
+  int n;
+  double rho, one_minus_rho, lr1, lr2;
+  long long split;
+  int init, filtered, mask;  // mask: CFA_TF1_STATE_F32 | CFA_TF1_GRAD_F32 | CFA_TF1_W_F32
+};
+// Python-float scalar times an array, in the array's dtype (numpy 2: the scalar is weak).
+__device__ __forceinline__ double scale(double c, double x, bool f32) {
+  return f32 ? (double)((float)c * (float)x) : c * x;
+}
+// cfa_ge_2stage.py:331-371 / :593-621 with numpy 2 promotion per operation:
+//   s_j = rho*g_j + (1-rho)*s_j (or g_j at init), stored in the state array's dtype;
+//   W   = W - lr*(filtered ? s_j : g_j).
+// Each product is computed in its array's dtype; a sum or difference is fp32 only when both
+// operands are fp32, and W stays fp32 only while every update it receives is fp32.
+__global__ __launch_bounds__(kBlock) void mewma_tf1_f64_kernel(MewmaF64Args a, long long P) {
+  const bool s32 = a.mask & CFA_TF1_STATE_F32, g32 = a.mask & CFA_TF1_GRAD_F32;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
+       i += (long long)gridDim.x * kBlock) {
+    double W = a.W[i];
+    bool w32 = a.mask & CFA_TF1_W_F32;
+    const double lr = i < a.split ? a.lr1 : a.lr2;
+    for (int j = 0; j < a.n; ++j) {
+      const double g = a.g[j][i * a.gstride[j]];
+      double s;
+      if (a.init) {
+        s = g;
+      } else {
+        const double t1 = scale(a.rho, g, g32);
+        const double t2 = scale(a.one_minus_rho, a.s[j][i], s32);
+        s = (g32 && s32) ? (double)((float)t1 + (float)t2) : t1 + t2;
+      }
+      if (s32) s = (double)(float)s;
+      a.s[j][i] = s;
+      const bool u32 = a.filtered ? s32 : g32;
+      const double t = scale(lr, a.filtered ? s : g, u32);
+      if (w32 && u32) {
+        W = (double)((float)W - (float)t);
+      } else {
+        W = W - t;
+        w32 = false;
+      }
+    }
+    a.W[i] = W;
+  }
+}
+
+template <bool FROM64, bool TO64>
+static void launch_tf1_vec(int n, unsigned grid, hipStream_t st, void* out, const Tf1Fanin& f,
+                           long long nvec, const CompressParams& cp, int compress) {
+#define CFA_CASE(K) \
+  case K:           \
+    mix_tf1_vec_kernel<K, FROM64, TO64><<<grid, kBlock, 0, st>>>(out, f, nvec, cp, compress); \
+    break;
+  switch (n) {
+    CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6) CFA_CASE(7)
+    CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13) CFA_CASE(14)
+    CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
+// One TF1 pass of 1..CFA_MAX_FANIN neighbours over [0, P): `head` scalar elements, a float4
+// body of nvec vectors, a scalar tail. out is fp32 (last pass) or the fp64 scratch.
+static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
+                    const float* const* nbrs, const double* a, int m, size_t P, size_t head,
+                    size_t nvec, const CompressParams& cp, int compress, hipStream_t st) {
+  auto fanin_at = [&](size_t b) {
+    Tf1Fanin f{};
+    f.local = local + b;
+    f.w64 = w64 ? w64 + b : nullptr;
+    for (int j = 0; j < m; ++j) {
+      f.src[j] = nbrs[j] + b;
+      f.a[j] = a[j];
+    }
+    return f;
+  };
+  auto out_at = [&](size_t b) -> void* {
+    return to64 ? (void*)((double*)out + b) : (void*)((float*)out + b);
+  };
+  auto shifted = [&](size_t b) {
+    CompressParams c = cp;
+    c.cbegin = cp.cbegin - (long long)b;
+    c.cend = cp.cend - (long long)b;
+    return c;
+  };
+  if (nvec > 0) {
+    const Tf1Fanin f = fanin_at(head);
+    const unsigned grid = grid_for(((long long)nvec + kBlock - 1) / kBlock);
+    const CompressParams c = shifted(head);
+    void* o = out_at(head);
+    if (!w64 && !to64) launch_tf1_vec<false, false>(m, grid, st, o, f, (long long)nvec, c, compress);
+    else if (!w64 && to64) launch_tf1_vec<false, true>(m, grid, st, o, f, (long long)nvec, c, compress);
+    else if (w64 && to64) launch_tf1_vec<true, true>(m, grid, st, o, f, (long long)nvec, c, compress);
+    else launch_tf1_vec<true, false>(m, grid, st, o, f, (long long)nvec, c, compress);
+    if (int rc = check_launch("mix_tf1_vec")) return rc;
+  }
+  const size_t tail_begin = head + nvec * 4;
+  const size_t pieces[2][2] = {{0, head}, {tail_begin, P}};
+  for (auto& pc : pieces) {
+    const size_t b = pc[0], e = pc[1];
+    if (e <= b) continue;
+    const long long len = (long long)(e - b);
+    mix_tf1_scalar_kernel<<<grid_for((len + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        out_at(b), to64 ? 1 : 0, fanin_at(b), m, len, shifted(b), compress);
+    if (int rc = check_launch("mix_tf1_scalar")) return rc;
+  }
+  return CFA_OK;
+}
+
+}  // namespace
+
+extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* const* nbrs,
+                               const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                               size_t cend, unsigned long long* kept_count, void* stream) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  // With a counter the epilogue runs (mode 0 keeps, and counts, every element of the range).
+  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
+  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  cp.cbegin = (long long)cbegin;
+  cp.cend = (long long)cend;
+  cp.kept = kept_count;
+  const int compress = kept_count ? 1 : 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    // No neighbour: the bucket is the local model (fp32), then the epilogue (cfa_ongraphs.py:218-223).
+    if (out != local && P > 0)
+      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (!compress) return CFA_OK;
+    return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin, kept_count,
+                                     stream);
+  }
+  if (P == 0) return CFA_OK;
+  // Body/head/tail split shared by every pass (fp32 pointers decide it; the fp64 scratch is
+  // indexed like the bucket and only needs 8-byte alignment).
+  const uintptr_t mis = addr(out) & 15;
+  bool same = (addr(local) & 15) == mis;
+  for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
+  size_t head = P, nvec = 0;
+  if (same && (mis & 3) == 0) {
+    head = mis ? (16 - mis) / 4 : 0;
+    if (head > P) head = P;
+    nvec = (P - head) / 4;
+  }
+  double* scratch = nullptr;
+  if (n > CFA_MAX_FANIN)
+    CFA_HIP_CHECK(hipMallocAsync((void**)&scratch, P * sizeof(double), st));
+  int rc = CFA_OK;
+  for (int done = 0; done < n && rc == CFA_OK;) {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    const bool last = done + m == n;
+    rc = tf1_pass(last ? (void*)out : (void*)scratch, !last, local, done ? scratch : nullptr,
+                  nbrs + done, alphas + done, m, P, head, nvec, cp, last ? compress : 0, st);
+    done += m;
+  }
+  if (scratch) {
+    hipError_t e = hipFreeAsync(scratch, st);
+    if (rc == CFA_OK && e != hipSuccess) return fail(CFA_E_HIP, "hipFreeAsync: %s", hipGetErrorString(e));
+  }
+  return rc;
+}
+
+namespace {
+int fold_f64(double* out, const double* local, const double* const* nbrs, const double* alphas,
+             const double* divisors, int n, int rule, int step0_f32, size_t P, int mode,
+             size_t cbegin, size_t cend, unsigned long long* kept_count, hipStream_t st) {
+  if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
+  if (n > 0 && (!alphas || !nbrs)) return fail(CFA_E_INVALID, "null alphas/neighbour table");
+  if (rule == CFA_RULE_SEQUENTIAL_DIV && n > 0 && !divisors) return fail(CFA_E_INVALID, "null divisors");
+  if (rule != CFA_RULE_SEQUENTIAL && rule != CFA_RULE_SEQUENTIAL_DIV && rule != CFA_RULE_ACCUMULATE)
+    return fail(CFA_E_INVALID, "rule %d has no fp64 fold", rule);
+  if (step0_f32 && rule != CFA_RULE_SEQUENTIAL)
+    return fail(CFA_E_INVALID, "step0_f32 applies to the sequential rule only");
+  if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "null kept_count");
+  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  if (P == 0) return CFA_OK;
+  if (!out || !local) return fail(CFA_E_INVALID, "null out/local bucket");
+  for (int j = 0; j < n; ++j) {
+    if (!nbrs[j]) return fail(CFA_E_INVALID, "null neighbour bucket %d", j);
+    if (nbrs[j] == out) return fail(CFA_E_INVALID, "output aliases neighbour %d", j);
+  }
+  const int compress = kept_count ? 1 : 0;
+  if (compress && out == local && n > CFA_MAX_FANIN && (mode == CFA_COMPRESS_SPARSE_DPCM ||
+                                                        mode == CFA_COMPRESS_SPARSE_DPCM_HI))
+    return fail(CFA_E_INVALID, "in-place DPCM compression needs fan-in <= %d", CFA_MAX_FANIN);
+  cp.cbegin = (long long)cbegin;
+  cp.cend = (long long)cend;
+  cp.kept = kept_count;
+  const unsigned grid = grid_for(((long long)P + kBlock - 1) / kBlock);
+  int done = 0;
+  const double* w = local;
+  do {  // n == 0 runs one pass that copies local (and applies the epilogue)
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    const bool last = done + m == n;
+    F64Fanin f{};
+    f.src[0] = w;
+    f.m = m;
+    for (int j = 0; j < m; ++j) {
+      f.src[j + 1] = nbrs[done + j];
+      f.a[j + 1] = alphas[done + j];
+      f.d[j + 1] = divisors ? divisors[done + j] : 1.0;
+    }
+    mix_tf1_f64_kernel<<<grid, kBlock, 0, st>>>(out, f, (long long)P, rule,
+                                                done == 0 ? step0_f32 : 0, local, cp,
+                                                last ? compress : 0);
+    if (int rc = check_launch("fold_f64")) return rc;
+    done += m;
+    w = out;
+  } while (done < n);
+  return CFA_OK;
+}
+}  // namespace
+
+extern "C" int cfa_mix_tf1_f64(double* out, const double* local, const double* const* nbrs,
+                               const double* alphas, int n, int step0_f32, size_t P, int mode,
+                               size_t cbegin, size_t cend, unsigned long long* kept_count,
+                               void* stream) {
+  return fold_f64(out, local, nbrs, alphas, nullptr, n, CFA_RULE_SEQUENTIAL, step0_f32, P, mode,
+                  cbegin, cend, kept_count, (hipStream_t)stream);
+}
+
+extern "C" int cfa_fold_f64(double* out, const double* local, const double* const* nbrs,
+                            const double* alphas, const double* divisors, int n, int rule,
+                            size_t P, void* stream) {
+  return fold_f64(out, local, nbrs, alphas, divisors, n, rule, 0, P, CFA_COMPRESS_NONE, 0, 0,
+                  nullptr, (hipStream_t)stream);
+}
+
+extern "C" int cfa_mewma_tf1_f64(double* W, double* const* s, const double* const* g,
+                                 const int64_t* g_stride, int n, double rho, double lr1,
+                                 double lr2, size_t lr_split, int init, int use_filtered,
+                                 int f32_mask, size_t P, void* stream) {
+  if (n < 0) return fail(CFA_E_INVALID, "negative fan-in %d", n);
+  if (n > 0 && (!s || !g)) return fail(CFA_E_INVALID, "null state/gradient table");
+  if (f32_mask & ~(CFA_TF1_STATE_F32 | CFA_TF1_GRAD_F32 | CFA_TF1_W_F32))
+    return fail(CFA_E_INVALID, "unknown dtype mask bits 0x%x", f32_mask);
+  if (P == 0 || n == 0) return CFA_OK;
+  if (!W) return fail(CFA_E_INVALID, "null W");
+  hipStream_t st = (hipStream_t)stream;
+  for (int done = 0; done < n;) {
+    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
+    MewmaF64Args a{};
+    a.W = W;
+    a.n = m;
+    for (int j = 0; j < m; ++j) {
+      if (!s[done + j] || !g[done + j]) return fail(CFA_E_INVALID, "null state/gradient %d", done + j);
+      const long long gs = g_stride ? (long long)g_stride[done + j] : 1;
+      if (gs < 1) return fail(CFA_E_INVALID, "gradient stride %lld < 1", gs);
+      a.s[j] = s[done + j];
+      a.g[j] = g[done + j];
+      a.gstride[j] = gs;
+    }
+    a.rho = rho;
+    a.one_minus_rho = 1.0 - rho;  // Python: (1 - self.mewma)
+    a.lr1 = lr1;
+    a.lr2 = lr2;
+    a.split = (long long)lr_split;
+    a.init = init;
+    a.filtered = use_filtered;
+    a.mask = f32_mask;
+    mewma_tf1_f64_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        a, (long long)P);
+    if (int rc = check_launch("mewma_tf1_f64")) return rc;
+    done += m;
+  }
+  return CFA_OK;
+}
+

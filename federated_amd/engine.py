@@ -1,7 +1,7 @@
 """Device-level consensus engine: the libcfa kernels on PyTorch-ROCm tensors.
 
 PyTorch provides device memory and streams only; all arithmetic runs in the HIP kernels of
-``libcfa.so`` (``federated_amd/csrc/cfa_engine.hip``). Every call is asynchronous on the
+``libcfa.so`` (``federated_amd/csrc/cfa_*.hip``). Every call is asynchronous on the
 given stream (default: torch's current stream on the tensor's device).
 
 A *bucket* is a 1-D contiguous fp32 CUDA tensor holding one model (or gradient) flattened

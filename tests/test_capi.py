@@ -31,6 +31,8 @@ def test_library_exports_every_header_symbol():
                          check=True).stdout
     exported = set(re.findall(r"\sT\s+(cfa_\w+)", out))
     assert set(header_symbols()) <= exported
+    # ... and nothing else: measurement-only kernels live in libcfa_exp.so, not in the product
+    assert exported == set(header_symbols()), sorted(exported - set(header_symbols()))
     for name in header_symbols():
         assert hasattr(lib, name)
 

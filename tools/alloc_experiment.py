@@ -17,7 +17,7 @@ from federated_amd.engine import get_engine  # noqa: E402
 
 P, L, R, REPS = 25_000_000, 16, 5, int(os.environ.get("ALLOC_REPS", "3"))
 eng = get_engine(0)
-lib = _lib.load()
+lib = _lib.load_experiments()
 lib.cfa_experimental_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
 lib.cfa_experimental_free.argtypes = [ctypes.c_void_p]
 a = [1.0 / 9] * 8
@@ -30,7 +30,7 @@ class Raw:
         self.ptr = ctypes.c_void_p()
         rc = lib.cfa_experimental_malloc(ctypes.byref(self.ptr), n * 4, flags)
         if rc:
-            raise RuntimeError(lib.cfa_last_error())
+            raise RuntimeError(lib.cfa_exp_last_error())
         self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (self.ptr.value, False),
                                          "version": 3, "strides": None}
 

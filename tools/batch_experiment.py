@@ -18,7 +18,7 @@ from federated_amd.engine import get_engine  # noqa: E402
 
 P, L, R, MIXES = 25_001_984, 16, 5, 32
 eng = get_engine(0)
-lib = _lib.load()
+lib = _lib.load_experiments()
 fn = lib.cfa_experimental_mix8_batch
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_float),
@@ -44,7 +44,7 @@ def mix(v, i):
         b, soft = v[1]
         rc = fn(o[i].data_ptr(), m[i].data_ptr(), _lib.ptr_table([x.data_ptr() for x in nbrs(i)]), al, P, b, soft,
                 spin, 2, st)
-        assert rc == 0, lib.cfa_last_error()
+        assert rc == 0, lib.cfa_exp_last_error()
 
 
 ref = torch.empty(P, device="cuda")

@@ -17,7 +17,7 @@ from federated_amd.engine import get_engine  # noqa: E402
 
 P, L, R, MIXES = 25_001_984, 16, 5, 32
 eng = get_engine(0)
-lib = _lib.load()
+lib = _lib.load_experiments()
 fn = lib.cfa_experimental_mix8_traverse
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_float),
@@ -36,7 +36,7 @@ def run(v):
         i = k % L
         nb = [m[(i + d) % L] for d in (-4, -3, -2, -1, 1, 2, 3, 4)]
         rc = fn(o[i].data_ptr(), m[i].data_ptr(), _lib.ptr_table([x.data_ptr() for x in nb]), al, P, v[1], v[2], st)
-        assert rc == 0, lib.cfa_last_error()
+        assert rc == 0, lib.cfa_exp_last_error()
 
 
 times = {v[0]: [] for v in variants}

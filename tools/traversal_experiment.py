@@ -17,7 +17,7 @@ from federated_amd.engine import get_engine  # noqa: E402
 
 P, L, R, STACKS, MIXES = 25_001_984, 16, 4, 5, 32
 eng = get_engine(0)
-lib = _lib.load()
+lib = _lib.load_experiments()
 fn = lib.cfa_experimental_mix8_traverse
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_float),
@@ -39,7 +39,7 @@ def mix(v, m, o, i):
         eng.mix_seq(o[i], m[i], nbrs(m, i), alphas)
     else:
         rc = fn(o[i].data_ptr(), m[i].data_ptr(), _lib.ptr_table([x.data_ptr() for x in nbrs(m, i)]), al, P, v[1], v[2], st)
-        assert rc == 0, lib.cfa_last_error()
+        assert rc == 0, lib.cfa_exp_last_error()
 
 
 m0, o0 = stacks[0]

@@ -16,7 +16,7 @@ from federated_amd.engine import get_engine  # noqa: E402
 
 P, K, ROUNDS, LAUNCH = 25_001_984, 8, 5, 8  # P multiple of 4096
 eng = get_engine(0)
-lib = _lib.load()
+lib = _lib.load_experiments()
 fn = lib.cfa_experimental_mix8_buf
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_float),
@@ -42,7 +42,7 @@ def launch(c, s):
     else:
         rc = fn(out.data_ptr(), loc.data_ptr(), _lib.ptr_table([x.data_ptr() for x in nb]), _lib.float_array(alphas),
                 P, c[1], c[2], c[3], st)
-        assert rc == 0, lib.cfa_last_error()
+        assert rc == 0, lib.cfa_exp_last_error()
 
 
 times = {c: [] for c in cfgs}
