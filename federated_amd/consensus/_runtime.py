@@ -69,6 +69,10 @@ def savemat_retry(path: str, data: dict) -> None:
         sio.savemat(path, data)
 
 
+PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
+PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
+
+
 class HostMixer:
     """Host arrays in, host arrays out; the arithmetic runs in libcfa on the GPU."""
 
@@ -116,9 +120,14 @@ class HostMixer:
         Host path: the local and all neighbour buckets are packed into ONE cached
         pinned staging buffer and moved by one async H2D copy; the result (and the kept count)
         come back by async D2H into pinned memory; one stream synchronisation per call.
-        Returns (fp32 arrays with the local shapes, kept count or None)."""
+        Returns (fp32 arrays with the local shapes, kept count or None).
+
+        Buckets above PIPELINE_MIN_BYTES of staging (without compression or the TF1 rule) take
+        the chunked pipeline ``_mix_pipelined`` instead: same kernels per chunk, same results."""
         layout = BucketLayout.of(local)
         P, n = layout.P, len(nbrs)
+        if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
+            return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
         st = self._stream()
         with torch.cuda.stream(st):
             host = self._cached("h_in", (n + 1) * P, pinned=True)
@@ -159,6 +168,91 @@ class HostMixer:
             flat = h_out.numpy().copy()  # the pinned buffer is reused by the next call
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
+
+    def _aux_streams(self):
+        s = getattr(self._tls, "aux", None)
+        if s is None:
+            dev = self.engine.device
+            s = self._tls.aux = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+        return s
+
+    def _mix_pipelined(self, layout: BucketLayout, local, nbrs, alphas, divisors) -> List[np.ndarray]:
+        """Large host-resident mix as a chunk pipeline over three streams. Staging is
+        chunk-major: chunk c holds the n + 1 slices [a_c, b_c) of every bucket back to back
+        (each padded to a multiple of 4 elements, so every slice stays 16-byte aligned), so each
+        chunk is ONE H2D copy. The host packs chunk c + 1 (torch's parallel copy) while chunk c
+        is in flight; the mix of chunk c waits for its copy; its D2H waits for the mix."""
+        P, n = layout.P, len(nbrs)
+        C = max(2, min(32, -(-(n + 1) * P * 4 // PIPELINE_CHUNK_BYTES)))
+        step = -(-P // C)
+        step += (-step) % 4
+        bounds = [(a, min(a + step, P)) for a in range(0, P, step)]
+        pad = lambda m: m + (-m) % 4
+        offs, total = [], 0
+        for a, b in bounds:
+            offs.append(total)
+            total += (n + 1) * pad(b - a)
+        h2d, d2h = self._aux_streams()
+        comp = self._stream()
+        host = self._cached("h_pipe", total, pinned=True)
+        dev = self._cached("d_pipe", total)
+        d_out = self._cached("d_out", P)
+        h_out = self._cached("h_out", P, pinned=True)
+        models = [local] + list(nbrs)
+        flat = [[torch.from_numpy(np.ascontiguousarray(np.asarray(t)).reshape(-1)) for t in m] for m in models]
+        seg = [layout.segment(k) for k in range(len(layout.sizes))]
+        outs = [np.empty(shp, dtype=np.float32) for shp in layout.shapes]
+        out_flat = [torch.from_numpy(o.reshape(-1)) for o in outs]
+
+        def pieces(a, b):  # (layer k, [x, y) global, [x - lo, y - lo) within the layer)
+            for k, (lo, hi) in enumerate(seg):
+                x, y = max(a, lo), min(b, hi)
+                if x < y:
+                    yield k, x, y, lo
+
+        def unpack(c):
+            a, b = bounds[c]
+            done[c].synchronize()
+            for k, x, y, lo in pieces(a, b):
+                out_flat[k][x - lo:y - lo].copy_(h_out[x:y])
+
+        def prefault(c):  # first touch of the fresh output pages, off the critical path
+            a, b = bounds[c]
+            for k, x, y, lo in pieces(a, b):
+                out_flat[k][x - lo:y - lo].zero_()
+
+        done, unpacked = [], 0
+        for c, ((a, b), o) in enumerate(zip(bounds, offs)):
+            w = pad(b - a)
+            for j in range(n + 1):  # pack chunk c of every bucket (parallel copies)
+                base = o + j * w
+                for k, x, y, lo in pieces(a, b):
+                    host[base + x - a:base + y - a].copy_(flat[j][k][x - lo:y - lo])
+            with torch.cuda.stream(h2d):
+                dev[o:o + (n + 1) * w].copy_(host[o:o + (n + 1) * w], non_blocking=True)
+            comp.wait_stream(h2d)
+            src = [dev[o + j * w:o + j * w + (b - a)] for j in range(n + 1)]
+            if divisors is not None:
+                self.engine.mix_seq_div(d_out[a:b], src[0], src[1:], list(alphas), list(divisors), stream=comp)
+            else:
+                self.engine.mix_seq(d_out[a:b], src[0], src[1:], list(alphas), stream=comp)
+            d2h.wait_stream(comp)
+            with torch.cuda.stream(d2h):
+                h_out[a:b].copy_(d_out[a:b], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(d2h)
+            done.append(ev)
+            # host work while this chunk's H2D is in flight: fault in this chunk's output pages,
+            # and unpack whatever result chunks have already landed (never block on a D2H: the
+            # copy queue may order it behind the in-flight H2D)
+            prefault(c)
+            while unpacked < c and done[unpacked].query():
+                unpack(unpacked)
+                unpacked += 1
+        while unpacked < len(bounds):
+            unpack(unpacked)
+            unpacked += 1
+        return outs
 
     def compress(self, y: np.ndarray, ref: Optional[np.ndarray], mode: int) -> Tuple[np.ndarray, int]:
         """Standalone compression epilogue (cfa_ongraphs.py:225-273) on one tensor."""

@@ -89,8 +89,9 @@ class DeviceBuckets:
 
 def measure_e2e(engine: Engine, P: int, K: int, reps: int = 5, chunks: int = 8) -> dict:
     """Host-resident CFA mix (buckets start and end in pinned host memory): H2D of K+1 buckets,
-    mix, D2H of the output. Reports (a) the serial form and (b) a chunked pipeline that overlaps
-    H2D of chunk c+1, the mix of chunk c and D2H of chunk c-1 on separate streams."""
+    mix, D2H of the output. Reports (a) the serial form and (b) a chunked pipeline (chunk-major
+    staging, one H2D per chunk) that overlaps H2D of chunk c+1, the mix of chunk c and D2H of
+    chunk c-1 on separate streams."""
     dev = engine.device
     host_in = [torch.empty(P, dtype=torch.float32, pin_memory=True).normal_() for _ in range(K + 1)]
     host_out = torch.empty(P, dtype=torch.float32, pin_memory=True)
@@ -105,27 +106,36 @@ def measure_e2e(engine: Engine, P: int, K: int, reps: int = 5, chunks: int = 8) 
         engine.mix_seq(d_out, d_in[0], d_in[1:], alphas, s)
         host_out.copy_(d_out, non_blocking=True)
 
+    # Pipelined form: chunk-major pinned staging (chunk c = the K+1 slices [a_c, b_c) back to
+    # back), so each chunk is ONE H2D copy; the mix of chunk c waits for its copy, its D2H for
+    # the mix, on three streams.
     h2d, k2, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    bounds = np.linspace(0, P, chunks + 1).astype(np.int64)
-    bounds = [(int(a) // 4 * 4, int(b) // 4 * 4 if i < chunks - 1 else P)
-              for i, (a, b) in enumerate(zip(bounds[:-1], bounds[1:]))]
+    step = -(-P // chunks)
+    step += (-step) % 4
+    bounds = [(a, min(a + step, P)) for a in range(0, P, step)]
+    pad = lambda m: m + (-m) % 4
+    offs, total = [], 0
+    for a, b in bounds:
+        offs.append(total)
+        total += (K + 1) * pad(b - a)
+    host_stage = torch.empty(total, dtype=torch.float32, pin_memory=True)
+    dev_stage = torch.empty(total, dtype=torch.float32, device=dev)
+    for (a, b), o in zip(bounds, offs):
+        w = pad(b - a)
+        for j, h in enumerate(host_in):
+            host_stage[o + j * w:o + j * w + (b - a)].copy_(h[a:b])
 
     def pipelined():
-        s_ev = []
-        for (a, b) in bounds:
+        for (a, b), o in zip(bounds, offs):
+            w = pad(b - a)
             with torch.cuda.stream(h2d):
-                for h, d in zip(host_in, d_in):
-                    d[a:b].copy_(h[a:b], non_blocking=True)
-                e = torch.cuda.Event()
-                e.record(h2d)
-            k2.wait_event(e)
-            engine.mix_seq(d_out[a:b], d_in[0][a:b], [x[a:b] for x in d_in[1:]], alphas, k2)
-            e2 = torch.cuda.Event()
-            e2.record(k2)
-            d2h.wait_event(e2)
+                dev_stage[o:o + (K + 1) * w].copy_(host_stage[o:o + (K + 1) * w], non_blocking=True)
+            k2.wait_stream(h2d)
+            src = [dev_stage[o + j * w:o + j * w + (b - a)] for j in range(K + 1)]
+            engine.mix_seq(d_out[a:b], src[0], src[1:], alphas, k2)
+            d2h.wait_stream(k2)
             with torch.cuda.stream(d2h):
                 host_out[a:b].copy_(d_out[a:b], non_blocking=True)
-            s_ev.append(e2)
 
     res = {}
     for name, fn in (("serial", serial), ("pipelined", pipelined)):

@@ -204,3 +204,27 @@ def test_population_round_window_path_equals_csr(gpu, D, P, hl, hr):
     h = models.cpu().numpy()
     for d in (0, D // 2, D - 1):
         assert np.array_equal(win.out[d].cpu().numpy(), sequential_mix(h[d], [h[j] for j in lists[d]], T.alphas_tf2(lists[d], d, D)))
+
+
+@pytest.mark.parametrize("divide", [False, True])
+def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide):
+    """HostMixer.mix's chunked pipeline (chunk-major staging, one H2D per chunk, three streams)
+    returns the single-shot result bit for bit, across layer boundaries and ragged tails."""
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(21)
+    shapes = [(1001, 333), (333,), (517, 129), (7,)]
+    local = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    nbrs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(3)]
+    al = [0.25, 0.5, 0.125]
+    div = [4.0, 4.0, 4.0] if divide else None
+    mx = R.mixer()
+    ref, _ = mx.mix(local, nbrs, al, divisors=div)  # single shot (below the default threshold)
+    monkeypatch.setattr(R, "PIPELINE_MIN_BYTES", 1 << 20)
+    monkeypatch.setattr(R, "PIPELINE_CHUNK_BYTES", 600_000)
+    got, kept = mx.mix(local, nbrs, al, divisors=div)
+    assert kept is None
+    for a, r, s in zip(got, ref, shapes):
+        assert a.shape == s and a.dtype == np.float32 and np.array_equal(a, r)
+    flat = lambda m: np.concatenate([x.reshape(-1) for x in m])
+    if not divide:
+        assert np.array_equal(flat(got), sequential_mix(flat(local), [flat(m) for m in nbrs], al))
