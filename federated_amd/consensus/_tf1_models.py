@@ -66,3 +66,27 @@ def gradients(ml_model: int, x, y, W1, b1, W2, b2, stride: int = 1, device=None)
         raise ValueError("Unable to set the ML model paramters")
     g = torch.autograd.grad(_cost(logits, yy), params)
     return [gi.detach().cpu().numpy() for gi in g]
+
+
+def gradients_batched(ml_model: int, x, y, models, stride: int = 1, device=None):
+    """``gradients`` for several models at once (the CFA-GE neighbour-gradient
+    evaluation batched on the GPU): the device's cost at every neighbour model in ONE vectorised
+    forward/backward (torch.func.vmap over the stacked parameters). ``models`` = list of
+    (W1, b1, W2, b2). Returns one list of four fp32 arrays per model, as ``gradients`` does."""
+    from torch.func import grad, vmap
+    if not models:
+        return []
+    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float32), device=dev)
+    stack = lambda k, flat: torch.stack([t(np.squeeze(m[k])).reshape(-1) if flat else t(m[k]) for m in models])
+    params = (stack(0, False), stack(1, True), stack(2, False), stack(3, True))
+    xx, yy = t(x), t(y)
+    if ml_model == 1:
+        fwd = lambda W1, b1, W2, b2: cnn_forward(xx, W1, b1, W2, b2, stride=stride)
+    elif ml_model == 2:
+        fwd = lambda W1, b1, W2, b2: nn2_forward(xx, W1, b1, W2, b2)
+    else:
+        raise ValueError("Unable to set the ML model paramters")
+    loss = lambda W1, b1, W2, b2: _cost(fwd(W1, b1, W2, b2), yy)
+    g = vmap(grad(loss, argnums=(0, 1, 2, 3)))(*params)
+    return [[gk[i].detach().cpu().numpy() for gk in g] for i in range(len(models))]

@@ -94,7 +94,8 @@ class CFA_ge_process:
         """Gradients of the local cost at each neighbour's datamat{j}_{model_epoch} model, in slot j
         of [..., devices] buckets, published as datagrad{ii}_{grad_epoch}.mat (:480-547)."""
         gv = [np.zeros(s) for s in self._grad_shapes()]
-        for j in nbr_vec:
+        models = []
+        for j in nbr_vec:  # the neighbours' models, loaded in the reference's order
             fname = "datamat{}_{}.mat".format(int(j), model_epoch)
             wait_for(fname)
             try:
@@ -102,9 +103,14 @@ class CFA_ge_process:
             except Exception:
                 pause(5)
                 content = loadmat_retry(fname)
-            model = [np.asarray(content["weights1"]), np.squeeze(np.asarray(content["biases1"])),
-                     np.asarray(content["weights2"]), np.squeeze(np.asarray(content["biases2"]))]
-            g = self._gradients(x, y, model)
+            models.append([np.asarray(content["weights1"]), np.squeeze(np.asarray(content["biases1"])),
+                           np.asarray(content["weights2"]), np.squeeze(np.asarray(content["biases2"]))])
+        if self.grad_fn is not None:
+            grads = [self._gradients(x, y, m) for m in models]
+        else:  # every neighbour model in one batched forward/backward (f3)
+            grads = _tf1_models.gradients_batched(self.ML_model, x, y, models,
+                                                  stride=getattr(self, "stride", 1))
+        for j, g in zip(nbr_vec, grads):
             for k in range(4):
                 gv[k][..., int(j)] = np.asarray(g[k]).reshape(gv[k].shape[:-1])
         path = "datagrad{}_{}.mat".format(self.ii_saved_local, grad_epoch)

@@ -1,6 +1,7 @@
 """The torch restatement of the two TF1 CFA-GE graphs (off the reduction path):
 autograd gradients against central finite differences in float64, on CPU."""
 import numpy as np
+import pytest
 import torch
 
 from federated_amd.consensus import _tf1_models as M
@@ -53,3 +54,26 @@ def test_same_padding_shapes_match_tf_rule():
     out = M.cnn_forward(x, torch.zeros(16, 1, 8), torch.zeros(8), torch.zeros(168, 8), torch.zeros(8), stride=5)
     assert out.shape == (2, 8)
     assert M._same_pad(512, 16, 5) == (7, 7) and M._same_pad(103, 5, 5) == (1, 1)
+
+
+@pytest.mark.parametrize("ml", [1, 2])
+def test_batched_gradients_match_per_model(ml):
+    """gradients_batched (all neighbour models in one vmapped forward/backward, f3) equals the
+    per-model evaluation within fp32 tolerance (1e-5 normwise per tensor)."""
+    import torch
+    from conftest import normwise_close
+    from federated_amd.consensus import _tf1_models as M
+    rng = np.random.default_rng(ml)
+    if ml == 1:
+        shapes, xdim, stride = [(16, 1, 8), (8,), (168, 8), (8,)], 512, 5
+    else:
+        shapes, xdim, stride = [(64, 16), (16,), (16, 8), (8,)], 64, 1
+    models = [[(rng.standard_normal(s) * 0.1).astype(np.float32) for s in shapes] for _ in range(4)]
+    x = rng.standard_normal((6, xdim)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[np.arange(6) % 8]
+    cpu = torch.device("cpu")
+    batched = M.gradients_batched(ml, x, y, models, stride=stride, device=cpu)
+    assert M.gradients_batched(ml, x, y, [], stride=stride, device=cpu) == []
+    for m, gb in zip(models, batched):
+        for a, r in zip(gb, M.gradients(ml, x, y, *m, stride=stride, device=cpu)):
+            assert a.shape == r.shape and normwise_close(a, r)
