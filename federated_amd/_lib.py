@@ -84,7 +84,30 @@ SIGNATURES = {
                                        _c_size_t, _c_void_p]),
     "cfa_allreduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
+    "cfa_payload_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
+    "cfa_payload_free": (None, [_c_void_p]),
+    "cfa_payload_num_keys": (_c_int, [_c_void_p]),
+    "cfa_payload_key": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_size_t)]),
+    "cfa_payload_info": (_c_int, [_c_void_p, ctypes.c_char_p, _c_int_p, _c_int_p, _c_int64_p, _c_int64_p]),
+    "cfa_payload_scalar": (_c_int, [_c_void_p, ctypes.c_char_p, _c_int_p, _c_int64_p,
+                                    ctypes.POINTER(ctypes.c_double)]),
+    "cfa_payload_read_f64": (_c_int, [_c_void_p, ctypes.c_char_p, _c_void_p, ctypes.c_int64]),
+    "cfa_payload_read_f32": (_c_int, [_c_void_p, ctypes.c_char_p, _c_void_p, ctypes.c_int64]),
+    "cfa_payload_encode": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_size_t,
+                                    ctypes.POINTER(_c_size_t)]),
 }
+
+CFA_PAYLOAD_MAX_DIM = 8
+PAYLOAD_NONE, PAYLOAD_BOOL, PAYLOAD_INT, PAYLOAD_FLOAT = 0, 1, 2, 3
+PAYLOAD_F32_ARRAY, PAYLOAD_F64_ARRAY, PAYLOAD_I64_ARRAY, PAYLOAD_BOOL_ARRAY = 4, 5, 6, 7
+PAYLOAD_STR, PAYLOAD_DICT = 8, 9
+
+
+class PayloadItem(ctypes.Structure):
+    """cfa_payload_item_t"""
+    _fields_ = [("key", ctypes.c_char_p), ("kind", ctypes.c_int), ("data", ctypes.c_void_p),
+                ("ndim", ctypes.c_int), ("shape", _c_int64_p), ("ivalue", ctypes.c_int64),
+                ("fvalue", ctypes.c_double)]
 
 class Launch(ctypes.Structure):
     """cfa_launch_t"""

@@ -330,7 +330,10 @@ class HostMixer:
             hv = host.numpy().reshape(n + 1, P)
             layout.pack(local, hv[0])
             for j, x in enumerate(nbrs):
-                layout.pack(x, hv[j + 1])
+                if callable(x):  # a filler writes the flat bucket itself (e.g. a payload decoder)
+                    x(hv[j + 1])
+                else:
+                    layout.pack(x, hv[j + 1])
             dev = self._cached("d_in64", (n + 1) * P, torch.float64)
             dev.copy_(host, non_blocking=True)
             d = dev.view(n + 1, P)
@@ -362,7 +365,9 @@ class HostMixer:
     def fold64(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float], rule: int,
                divisors: Optional[Sequence[float]] = None) -> List[np.ndarray]:
         """fp64 fold (``cfa_fold_f64``) of per-layer arrays widened to fp64 buckets; returns fp64
-        arrays with the local shapes. One H2D of all buckets, one launch, one D2H."""
+        arrays with the local shapes. One H2D of all buckets, one launch, one D2H. A neighbour
+        may be given as a callable ``fill(dst)`` that writes its flat fp64 bucket into the pinned
+        staging row ``dst`` (the MQTT payload decoder does)."""
         layout = BucketLayout.of(local)
         P, n = layout.P, len(nbrs)
         st = self._stream()
@@ -371,7 +376,10 @@ class HostMixer:
             hv = host.numpy().reshape(n + 1, P)
             layout.pack(local, hv[0])
             for j, x in enumerate(nbrs):
-                layout.pack(x, hv[j + 1])
+                if callable(x):  # a filler writes the flat bucket itself (e.g. a payload decoder)
+                    x(hv[j + 1])
+                else:
+                    layout.pack(x, hv[j + 1])
             dev = self._cached("d_in64", (n + 1) * P, torch.float64)
             dev.copy_(host, non_blocking=True)
             d = dev.view(n + 1, P)

@@ -23,11 +23,12 @@ from typing import List, Sequence
 
 import numpy as np
 
-from . import _lib
+from . import _lib, payload as _payload
 from .consensus._runtime import mixer
 
 __all__ = ["ps_mqtt_aggregate", "learner_consensus_mix", "cfa_fa_server_init", "cfa_fa_server_round",
-           "cfa_fa_client_mix"]
+           "cfa_fa_client_mix", "ps_mqtt_aggregate_payloads", "ps_mqtt_publish", "learner_consensus_receive",
+           "learner_publish"]
 
 
 def _shapes(local, nbrs):
@@ -101,6 +102,75 @@ def learner_consensus_mix(model_parameters: Sequence, rx_global_model: Sequence,
     (the reference's values: update_factor 1, active 2)."""
     return _fold(list(model_parameters), [list(rx_global_model)], [update_factor], _lib.RULE_SEQUENTIAL_DIV,
                  [active])
+
+
+def _payload_fills(local: Sequence, payloads: Sequence, prefix: str):
+    """Per payload, a filler that decodes its layers straight into a pinned fp64 staging row,
+    or None when a layer's shape differs from the local one (numpy would broadcast: decode to
+    arrays and take the general fold instead)."""
+    keys = _payload.layer_keys(prefix, len(local))
+    parsed = [p if isinstance(p, _payload.Payload) else _payload.Payload(p) for p in payloads]
+    for p in parsed:
+        for k, key in enumerate(keys):
+            kind, shape = p.info(key)
+            if kind == _lib.PAYLOAD_BOOL_ARRAY:
+                raise TypeError(f"{key}: boolean layer")  # numpy refuses bool - float subtraction
+            if shape != np.shape(local[k]):
+                return parsed, None
+    return parsed, [lambda dst, p=p: p.read_into(keys, dst) for p in parsed]
+
+
+def ps_mqtt_aggregate_payloads(model_parameters: Sequence, payloads: Sequence, update_factor: float,
+                               active: int, prefix: str = "model_layer") -> List[np.ndarray]:
+    """PS_server.py:90-118 + :130-133 from the raw MQTT payloads of the active devices, in
+    ``active_device_indexes`` order: each payload's ``model_layer{k}`` lists (what
+    ``np.asarray(st['model_layer{k}'])`` gives, fp64) are decoded by the native codec straight
+    into the pinned fp64 staging of the fold, then folded on the GPU as ``ps_mqtt_aggregate``
+    does. Returns the new model_parameters list (fp64, as the reference's before set_weights)."""
+    if len(payloads) != active:
+        raise ValueError("one payload per active device")
+    local = list(model_parameters)
+    parsed, fills = _payload_fills(local, payloads, prefix)
+    if fills is None:
+        keys = _payload.layer_keys(prefix, len(local))
+        return ps_mqtt_aggregate(local, [[p.array(k) for k in keys] for p in parsed], range(active),
+                                 update_factor, active)
+    return mixer().fold64(local, fills, [update_factor] * active, _lib.RULE_SEQUENTIAL_DIV, [active] * active)
+
+
+def ps_mqtt_publish(model_list: Sequence, epoch_count: int, training_end_signal: bool) -> bytes:
+    """PS_server.py:140-145: ``pickle.dumps({'global_model_layer{k}': w.tolist(), ...,
+    'global_epoch': epoch_count, 'training_end': training_end_signal})``, byte for byte."""
+    d = {f"global_model_layer{k}": np.asarray(w) for k, w in enumerate(model_list)}
+    d["global_epoch"] = int(epoch_count)
+    d["training_end"] = bool(training_end_signal)
+    return _payload.dumps(d)
+
+
+def learner_consensus_receive(model_parameters: Sequence, message_payload, update_factor: float = 1,
+                              active: int = 2, prefix: str = "model_layer"):
+    """learner_consensus.py:136-153 for one received payload: decode ``model_layer{k}`` and
+    ``local_epoch``; if ``training_end`` the received model replaces the local one (:146-147),
+    else ``p + update_factor * (rx - p) / active`` per layer on the GPU (:149-152). Returns
+    (new weights for set_weights, global_epoch, training_end)."""
+    p = message_payload if isinstance(message_payload, _payload.Payload) else _payload.Payload(message_payload)
+    keys = _payload.layer_keys(prefix, len(model_parameters))
+    global_epoch = p.scalar("local_epoch")
+    if p.scalar("training_end"):
+        return [p.array(k) for k in keys], global_epoch, True
+    local = list(model_parameters)
+    _, fills = _payload_fills(local, [p], prefix)
+    if fills is None:
+        return learner_consensus_mix(local, [p.array(k) for k in keys], update_factor, active), global_epoch, False
+    return (mixer().fold64(local, fills, [update_factor], _lib.RULE_SEQUENTIAL_DIV, [active]), global_epoch,
+            False)
+
+
+def learner_publish(model_list: Sequence, device_index: int, frame_count: int, epoch_count: int,
+                    training_end: bool) -> bytes:
+    """learner_consensus.py:261-268: the device's model payload, byte for byte."""
+    return _payload.model_payload(model_list, device=device_index, framecount=frame_count,
+                                  local_epoch=epoch_count, training_end=training_end)
 
 
 _KEYS = ("weights1", "biases1", "weights2", "biases2")

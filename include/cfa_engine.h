@@ -270,6 +270,69 @@ CFA_API int cfa_allreduce_sum_f32(void* comm, const float* send, float* recv, si
 CFA_API int cfa_reduce_sum_f32(void* comm, const float* send, float* recv, size_t count, int root,
                        void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * (f2) MQTT model payloads, host side. FL_over_MQTT ships models as
+ *   pickle.dumps({'model_layer{k}': w_k.tolist(), 'device': i, 'framecount': f,
+ *                 'local_epoch': e, 'training_end': b})
+ * (TF2/FL_over_MQTT/learner_consensus.py:257-268; PS_server.py:137-149 answers with
+ * 'global_model_layer{k}', 'global_epoch', 'training_end') and decodes them with
+ * pickle.loads + np.asarray (learner_consensus.py:136-144, PS_server.py:90-118).
+ * The codec below reads and writes those bytes without Python objects:
+ *   - decode: one structure pass over the payload, then the float runs of a key are
+ *     byte-swapped straight into a caller buffer (e.g. a pinned staging bucket), threaded for
+ *     large tensors. Values equal np.asarray(pickle.loads(payload)[key]) bit for bit (fp64), or
+ *     that array cast to fp32 (`_f32`). Only dict/list/str/int/bool/float/None and memo opcodes
+ *     are accepted; object-constructing opcodes (GLOBAL, REDUCE, BUILD, ...) are refused, so a
+ *     payload executes nothing. `buf` must stay alive and unchanged until cfa_payload_free.
+ *   - encode: the exact bytes of pickle.dumps(d, protocol) (CPython 3.10, framing included)
+ *     for d = {key: ndarray.tolist() | int | bool | float | None} in item order.
+ */
+typedef struct cfa_payload cfa_payload_t;  /* opaque parsed payload */
+#define CFA_PAYLOAD_MAX_DIM 8
+enum {
+  CFA_PAYLOAD_NONE = 0,
+  CFA_PAYLOAD_BOOL = 1,
+  CFA_PAYLOAD_INT = 2,
+  CFA_PAYLOAD_FLOAT = 3,
+  CFA_PAYLOAD_F32_ARRAY = 4,   /* encode only: float32 data, tolist() values */
+  CFA_PAYLOAD_F64_ARRAY = 5,   /* (nested) list whose np.asarray dtype is float64 */
+  CFA_PAYLOAD_I64_ARRAY = 6,   /* decode only: list of ints (np.asarray -> int64) */
+  CFA_PAYLOAD_BOOL_ARRAY = 7,  /* decode only: list of bools */
+  CFA_PAYLOAD_STR = 8,         /* decode only */
+  CFA_PAYLOAD_DICT = 9         /* decode only (nested dict; not readable as an array) */
+};
+typedef struct {
+  const char* key;       /* NUL-terminated UTF-8 */
+  int kind;              /* CFA_PAYLOAD_NONE .. CFA_PAYLOAD_F64_ARRAY */
+  const void* data;      /* arrays: C-contiguous host data of `shape` */
+  int ndim;              /* arrays: 0 .. CFA_PAYLOAD_MAX_DIM (0 = one float, as tolist()) */
+  const int64_t* shape;  /* arrays: ndim extents */
+  int64_t ivalue;        /* INT / BOOL */
+  double fvalue;         /* FLOAT */
+} cfa_payload_item_t;
+
+CFA_API int cfa_payload_parse(const void* buf, size_t len, cfa_payload_t** out);
+CFA_API void cfa_payload_free(cfa_payload_t* payload);
+/* Number of top-level keys; negative CFA_E* on error. */
+CFA_API int cfa_payload_num_keys(const cfa_payload_t* payload);
+/* Key `index` (insertion order) as a pointer into the payload bytes (not NUL-terminated). */
+CFA_API int cfa_payload_key(const cfa_payload_t* payload, int index, const char** key, size_t* len);
+/* Kind, shape (up to CFA_PAYLOAD_MAX_DIM extents) and element count of `key`'s value. */
+CFA_API int cfa_payload_info(const cfa_payload_t* payload, const char* key, int* kind, int* ndim,
+                             int64_t* shape, int64_t* numel);
+/* A scalar value (None / bool / int / float): ivalue for bool and int, fvalue for all. */
+CFA_API int cfa_payload_scalar(const cfa_payload_t* payload, const char* key, int* kind,
+                               int64_t* ivalue, double* fvalue);
+/* Row-major values of `key` (numel must match) into host memory. */
+CFA_API int cfa_payload_read_f64(const cfa_payload_t* payload, const char* key, double* dst,
+                                 int64_t numel);
+CFA_API int cfa_payload_read_f32(const cfa_payload_t* payload, const char* key, float* dst,
+                                 int64_t numel);
+/* Encode n items with pickle protocol 2..5. dst == NULL: only *size is set (the exact length).
+ * Otherwise dst must hold cap >= *size bytes (CFA_E_INVALID if not; *size is still set). */
+CFA_API int cfa_payload_encode(const cfa_payload_item_t* items, int n, int protocol, void* dst,
+                               size_t cap, size_t* size);
+
 #ifdef __cplusplus
 }
 #endif

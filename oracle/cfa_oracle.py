@@ -301,3 +301,53 @@ def cfa_fa_client_mix(W_val_l1, b_val_l1, W_val_l2, b_val_l2, mathcontent, eps_t
     W_val_l2 = W_val_l2 + eps_t_control2 * (np.array(mathcontent['weights2']) - W_val_l2)
     b_val_l2 = b_val_l2 + eps_t_control2 * (np.squeeze(np.asarray(mathcontent['biases2'])) - b_val_l2)
     return W_val_l1, b_val_l1, W_val_l2, b_val_l2
+
+
+# ----------------------------------------------------------------------------------------
+# (f2) MQTT payloads: the reference's own codec is CPython's stdlib pickle (3.10.12 here),
+# applied to the dicts the drivers build. These restate the driver lines with that codec.
+# ----------------------------------------------------------------------------------------
+
+
+def mqtt_learner_payload(model_list, device_index, frame_count, epoch_count, training_end) -> bytes:
+    """TF2/FL_over_MQTT/learner_consensus.py:260-268: layer lists via tolist(), then device,
+    framecount, local_epoch, training_end; pickle.dumps with the default protocol."""
+    import pickle
+    detObj = {}
+    for k in range(len(model_list)):
+        detObj['model_layer{}'.format(k)] = model_list[k].tolist()
+    detObj['device'] = device_index
+    detObj['framecount'] = frame_count
+    detObj['local_epoch'] = epoch_count
+    detObj['training_end'] = training_end
+    return pickle.dumps(detObj)
+
+
+def mqtt_ps_payload(model_list, epoch_count, training_end_signal) -> bytes:
+    """TF2/FL_over_MQTT/PS_server.py:140-145 (published at :146-149)."""
+    import pickle
+    detObj = {}
+    for k in range(len(model_list)):
+        detObj['global_model_layer{}'.format(k)] = model_list[k].tolist()
+    detObj['global_epoch'] = epoch_count
+    detObj['training_end'] = training_end_signal
+    return pickle.dumps(detObj)
+
+
+def mqtt_decode_layers(payload: bytes, layers: int, prefix: str = 'model_layer') -> list:
+    """learner_consensus.py:136-144 / PS_server.py:90, 116-117: pickle.loads, then
+    np.asarray per layer list (fp64 for tolist() floats)."""
+    import pickle
+    st = pickle.loads(payload)
+    return [np.asarray(st['{}{}'.format(prefix, k)]) for k in range(layers)]
+
+
+def mqtt_learner_receive(model_parameters, payload: bytes, layers: int):
+    """learner_consensus.py:136-153: decode; training_end -> the received model, else
+    p + 1 * (rx - p) / 2 per layer. Returns (weights, global_epoch, training_end)."""
+    import pickle
+    st = pickle.loads(payload)
+    rx = [np.asarray(st['model_layer{}'.format(k)]) for k in range(layers)]
+    if st['training_end']:
+        return rx, st['local_epoch'], True
+    return learner_consensus_mix(list(model_parameters), rx, 1, 2), st['local_epoch'], False
