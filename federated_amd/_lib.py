@@ -77,6 +77,10 @@ SIGNATURES = {
     "cfa_mix_window_f32": (_c_int, [_PP, _PP, _c_float_p, _c_int, _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_population_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         _c_int, _c_int, _c_size_t, _c_void_p]),
+    "cfa_ge_grad_cnn_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                     _c_void_p, _c_void_p, _c_int, _c_void_p]),
+    "cfa_ge_grad_2nn_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p, _c_void_p,
+                                     _c_int, _c_void_p]),
     "cfa_comm_unique_id": (_c_int, [_c_void_p]),
     "cfa_comm_init": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_void_p, _c_int]),
     "cfa_comm_destroy": (_c_int, [_c_void_p]),

@@ -48,6 +48,13 @@ def _check_bucket(t: torch.Tensor, name: str, P: Optional[int] = None, dtype=tor
     return n
 
 
+def _check_2d(t: torch.Tensor, name: str):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float32 or t.dim() != 2 \
+            or not t.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous 2-D fp32 CUDA tensor")
+    return int(t.shape[0]), int(t.shape[1])
+
+
 TF1_STATE_F32, TF1_GRAD_F32, TF1_W_F32 = 1, 2, 4  # cfa_mewma_tf1_f64 dtype mask
 
 
@@ -302,6 +309,41 @@ class Engine:
                   float(rho), float(lr1), float(lr2), int(lr_split), int(bool(init)),
                   int(bool(use_filtered)), P, self.stream_handle(stream))
         return W
+
+    # -- CFA-GE neighbour gradients (f3) ---------------------------------------------------
+    def _grad_args(self, x, y, models, grads):
+        B, L = _check_2d(x, "x")
+        By, C = _check_2d(y, "y")
+        M, P = _check_2d(models, "models")
+        if By != B:
+            raise ValueError("x and y must hold the same number of samples")
+        if tuple(grads.shape) != (M, P):
+            raise ValueError("grads must have the shape of models")
+        _check_2d(grads, "grads")
+        return B, L, C, M, P
+
+    def grad_cnn(self, x: torch.Tensor, y: torch.Tensor, models: torch.Tensor, grads: torch.Tensor,
+                 filter: int, number: int, stride: int, stream=None) -> torch.Tensor:
+        """Gradients of the CNN cost (cfa_ge_2stage.py:392-405, :425-430) at each row of
+        ``models`` [M, P] (TF1 bucket order W1 b1 W2 b2) into ``grads`` [M, P]."""
+        B, L, C, M, P = self._grad_args(x, y, models, grads)
+        L2 = -(-(-(-L // stride)) // stride)
+        if P != filter * number + number + L2 * number * C + C:
+            raise ValueError(f"CNN bucket of {P} parameters does not match filter {filter}, number {number}, "
+                             f"stride {stride}, {L} inputs, {C} classes (multip must be {L2})")
+        _lib.call("cfa_ge_grad_cnn_f32", x.data_ptr(), y.data_ptr(), B, L, C, int(filter), int(number),
+                  int(stride), models.data_ptr(), grads.data_ptr(), M, self.stream_handle(stream))
+        return grads
+
+    def grad_2nn(self, x: torch.Tensor, y: torch.Tensor, models: torch.Tensor, grads: torch.Tensor,
+                 hidden: int, stream=None) -> torch.Tensor:
+        """Gradients of the 2NN cost (cfa_ge_2stage.py:407-420, :425-430); see grad_cnn."""
+        B, L, C, M, P = self._grad_args(x, y, models, grads)
+        if P != L * hidden + hidden + hidden * C + C:
+            raise ValueError(f"2NN bucket of {P} parameters does not match {L} inputs, {hidden} hidden, {C} classes")
+        _lib.call("cfa_ge_grad_2nn_f32", x.data_ptr(), y.data_ptr(), B, L, int(hidden), C, models.data_ptr(),
+                  grads.data_ptr(), M, self.stream_handle(stream))
+        return grads
 
     # -- population ------------------------------------------------------------------------
     def mix_window(self, outs: Sequence[torch.Tensor], rows: Sequence[torch.Tensor], alphas: Sequence[Sequence[float]],

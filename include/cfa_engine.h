@@ -235,6 +235,24 @@ CFA_API int cfa_mewma_update_f32(float* W, float* const* s, const float* const* 
 CFA_API int cfa_mix_window_f32(float* const* out, const float* const* rows, const float* alphas,
                                int nb, int hl, int hr, size_t P, void* stream);
 
+/* (f3) CFA-GE neighbour-gradient evaluation: the gradient of a device's own cost at each of M
+ * neighbour models, for the two TF1 graphs of cfa_ge_2stage.py (:391-433 graph, :512-528 one
+ * Session per neighbour; cfa_ge_4stage.py the same), one workgroup per model, fp32 like the
+ * reference's placeholders. x [B, L] and y [B, classes] are the device's samples and one-hot
+ * labels (x_train2, y_train2); models [M, P] and grads [M, P] are model buckets in the TF1
+ * order (W1, b1, W2, b2), all device arrays.
+ *   CNN (ML_model 1): W1 [filter, 1, number], conv stride = pool size = `stride`, SAME padding,
+ *       W2 [L2 * number, classes] with L2 = ceil(ceil(L / stride) / stride) (the reference's
+ *       `multip`); P = filter*number + number + L2*number*classes + classes.
+ *   2NN (ML_model 2): W1 [L, hidden], W2 [hidden, classes]; P = L*hidden + hidden + hidden*classes + classes.
+ * cost = mean_b(-sum_c y log(clip(softmax, 1e-15, 0.99))) (:425-426). CFA_E_UNSUPPORTED when the
+ * activations of B samples do not fit one workgroup's LDS. */
+CFA_API int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L, int classes, int filter,
+                                int number, int stride, const float* models, float* grads, int M,
+                                void* stream);
+CFA_API int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, int hidden, int classes,
+                                const float* models, float* grads, int M, void* stream);
+
 /* (a1-a6 batched) Population round: one launch mixes D devices.
  * For device d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]) list its sources in order; the
  * FIRST entry is the device's own (local) bucket. Source e is src_ptrs[csr_idx[e]], output d

@@ -351,3 +351,94 @@ def mqtt_learner_receive(model_parameters, payload: bytes, layers: int):
     if st['training_end']:
         return rx, st['local_epoch'], True
     return learner_consensus_mix(list(model_parameters), rx, 1, 2), st['local_epoch'], False
+
+
+# ----------------------------------------------------------------------------------------
+# (f3) CFA-GE neighbour-gradient evaluation: the TF1 graphs of cfa_ge_2stage.py:391-433 with
+# their gradients derived by hand (float64, from the fp32 values the placeholders receive).
+# Pinned by central finite differences and by torch autograd in tests/test_tf1_models.py.
+# ----------------------------------------------------------------------------------------
+
+
+def _tf_same_left(L: int, k: int, s: int) -> int:
+    out = -(-L // s)
+    return max((out - 1) * s + k - L, 0) // 2
+
+
+def _softmax_xent_grad(logits, y):
+    """cost = mean_b(-sum_c y*log(clip(softmax, 1e-15, 0.99))) (:425-426) and d cost/d logits;
+    the clip passes the gradient where 1e-15 <= pred <= 0.99 (tf.clip_by_value)."""
+    z = logits - logits.max(axis=1, keepdims=True)
+    e = np.exp(z)
+    pred = e / e.sum(axis=1, keepdims=True)
+    B = logits.shape[0]
+    clipped = np.clip(pred, 1e-15, 0.99)
+    cost = np.mean(-np.sum(y * np.log(clipped), axis=1))
+    dpred = np.where((pred >= 1e-15) & (pred <= 0.99), -(y / clipped) / B, 0.0)
+    dlogits = (dpred - np.sum(dpred * pred, axis=1, keepdims=True)) * pred
+    return cost, dlogits
+
+
+def tf1_cnn_forward(x, W1, b1, W2, b2, stride):
+    """ML_model 1 (:392-405): conv1d SAME (stride S) + bias + relu -> max_pooling1d(S, S, SAME)
+    -> NWC flatten -> logits. Returns (logits, pooled [B, L2, NC], argmax positions)."""
+    x = np.asarray(x, np.float64)
+    W1 = np.asarray(W1, np.float64)
+    F, NC = W1.shape[0], W1.shape[2]
+    B, L = x.shape
+    S = int(stride)
+    L1 = -(-L // S)
+    L2 = -(-L1 // S)
+    pl, ql = _tf_same_left(L, F, S), _tf_same_left(L1, S, S)
+    xpad = np.zeros((B, (L1 - 1) * S + F))
+    lo = pl
+    xpad[:, lo:lo + L] = x[:, :max(0, min(L, xpad.shape[1] - lo))]
+    idx = np.arange(L1)[:, None] * S + np.arange(F)[None, :]          # [L1, F]
+    z = np.einsum("blf,fc->blc", xpad[:, idx], W1[:, 0, :]) + np.asarray(b1, np.float64).reshape(-1)
+    h = np.maximum(z, 0.0)                                             # [B, L1, NC]
+    pooled = np.empty((B, L2, NC))
+    arg = np.empty((B, L2, NC), dtype=np.int64)
+    for q in range(L2):
+        ps = [p for p in range(q * S - ql, q * S - ql + S) if 0 <= p < L1]
+        win = h[:, ps, :]
+        a = np.argmax(win, axis=1)                                     # first maximum
+        pooled[:, q, :] = np.take_along_axis(win, a[:, None, :], axis=1)[:, 0, :]
+        arg[:, q, :] = np.asarray(ps)[a]
+    fc = pooled.reshape(B, L2 * NC)
+    logits = fc @ np.asarray(W2, np.float64) + np.asarray(b2, np.float64).reshape(-1)
+    return logits, pooled, arg, (xpad, pl, L1)
+
+
+def tf1_cnn_grads(x, y, W1, b1, W2, b2, stride):
+    """d cost / d (W1, b1, W2, b2) of the CNN graph (:392-405, :425-430), float64."""
+    W1 = np.asarray(W1, np.float64)
+    W2 = np.asarray(W2, np.float64)
+    y = np.asarray(y, np.float64)
+    F, NC = W1.shape[0], W1.shape[2]
+    S = int(stride)
+    logits, pooled, arg, (xpad, pl, L1) = tf1_cnn_forward(x, W1, b1, W2, b2, stride)
+    B, L2, _ = pooled.shape
+    cost, dlog = _softmax_xent_grad(logits, y)
+    fc = pooled.reshape(B, -1)
+    gW2 = fc.T @ dlog
+    gb2 = dlog.sum(axis=0)
+    dfc = (dlog @ W2.T).reshape(B, L2, NC) * (pooled > 0)              # relu gradient at the max
+    gW1 = np.zeros((F, 1, NC))
+    for k in range(F):
+        xs = np.take_along_axis(xpad, (arg * S + k).reshape(B, -1), axis=1).reshape(B, L2, NC)
+        gW1[k, 0, :] = np.sum(dfc * xs, axis=(0, 1))
+    gb1 = dfc.sum(axis=(0, 1))
+    return [gW1, gb1, gW2, gb2], cost
+
+
+def tf1_2nn_grads(x, y, W1, b1, W2, b2):
+    """d cost / d (W1, b1, W2, b2) of the 2NN graph (:407-420, :425-430), float64."""
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    W1 = np.asarray(W1, np.float64)
+    W2 = np.asarray(W2, np.float64)
+    act = np.maximum(x @ W1 + np.asarray(b1, np.float64).reshape(-1), 0.0)
+    logits = act @ W2 + np.asarray(b2, np.float64).reshape(-1)
+    cost, dlog = _softmax_xent_grad(logits, y)
+    dz = (dlog @ W2.T) * (act > 0)
+    return [x.T @ dz, dz.sum(axis=0), act.T @ dlog, dlog.sum(axis=0)], cost

@@ -1,0 +1,83 @@
+"""(f3) HIP gradient kernels (cfa_ge_grad_cnn_f32 / cfa_ge_grad_2nn_f32) against the oracle's
+float64 gradients of the TF1 graphs (cfa_ge_2stage.py:391-433): fp32 kernels, tolerance
+1e-5 normwise per tensor (max|g - r| <= 1e-5 max|r|, the north-star fp32 bar)."""
+import numpy as np
+import pytest
+
+from conftest import normwise_close
+from oracle import cfa_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _cnn_models(rng, M, F=16, NC=8, LN=168, C=8):
+    return [[(rng.standard_normal((F, 1, NC)) * 0.3).astype(np.float32),
+             (rng.standard_normal(NC) * 0.1).astype(np.float32),
+             (rng.standard_normal((LN, C)) * 0.1).astype(np.float32),
+             (rng.standard_normal(C) * 0.1).astype(np.float32)] for _ in range(M)]
+
+
+def _check(got, models, ref_fn):
+    for g, m in zip(got, models):
+        ref, _ = ref_fn(m)
+        for a, r in zip(g, ref):
+            assert a.dtype == np.float32 and a.shape == r.shape
+            assert normwise_close(a, r, 1e-5), (np.abs(a - r).max(), np.abs(r).max())
+
+
+@pytest.mark.parametrize("B,M", [(24, 2), (24, 5), (1, 1), (100, 3)])  # 100: chunked through LDS
+def test_cnn_gradients_match_oracle(gpu, B, M):
+    from federated_amd.consensus import _tf1_models as T
+    rng = np.random.default_rng(B * 10 + M)
+    models = _cnn_models(rng, M)
+    x = rng.standard_normal((B, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[rng.integers(0, 8, B)]
+    got = T.gradients_batched(1, x, y, models, stride=5)
+    _check(got, models, lambda m: orc.tf1_cnn_grads(x, y, *m, stride=5))
+
+
+@pytest.mark.parametrize("L,S,F", [(100, 3, 5), (64, 2, 7), (37, 4, 4)])
+def test_cnn_other_geometries(gpu, L, S, F):
+    from federated_amd.consensus import _tf1_models as T
+    rng = np.random.default_rng(L)
+    L2 = -(-(-(-L // S)) // S)
+    models = _cnn_models(rng, 2, F=F, NC=6, LN=L2 * 6, C=5)
+    x = rng.standard_normal((9, L)).astype(np.float32)
+    y = np.eye(5, dtype=np.float32)[rng.integers(0, 5, 9)]
+    got = T.gradients_batched(1, x, y, models, stride=S)
+    _check(got, models, lambda m: orc.tf1_cnn_grads(x, y, *m, stride=S))
+
+
+@pytest.mark.parametrize("B,M", [(24, 2), (300, 2), (3, 4)])  # 300: chunked through LDS
+def test_2nn_gradients_match_oracle(gpu, B, M):
+    from federated_amd.consensus import _tf1_models as T
+    rng = np.random.default_rng(B + M)
+    models = [[(rng.standard_normal((512, 32)) * 0.1).astype(np.float32),
+               (rng.standard_normal(32) * 0.1).astype(np.float32),
+               (rng.standard_normal((32, 8)) * 0.3).astype(np.float32),
+               (rng.standard_normal(8) * 0.1).astype(np.float32)] for _ in range(M)]
+    x = rng.standard_normal((B, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[rng.integers(0, 8, B)]
+    got = T.gradients_batched(2, x, y, models)
+    _check(got, models, lambda m: orc.tf1_2nn_grads(x, y, *m))
+
+
+def test_saturated_softmax(gpu):
+    from federated_amd.consensus import _tf1_models as T
+    rng = np.random.default_rng(9)
+    models = _cnn_models(rng, 1)
+    models[0][3] = np.array([40, 0, 0, 0, 0, 0, 0, 0], np.float32)
+    x = rng.standard_normal((6, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[[0, 0, 1, 0, 2, 0]]
+    got = T.gradients_batched(1, x, y, models, stride=5)
+    _check(got, models, lambda m: orc.tf1_cnn_grads(x, y, *m, stride=5))
+
+
+def test_bad_geometry_is_refused(gpu):
+    from federated_amd.consensus import _tf1_models as T
+    rng = np.random.default_rng(1)
+    models = _cnn_models(rng, 1, LN=160)  # multip 20 != ceil(ceil(512/5)/5) = 21
+    x = rng.standard_normal((2, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[[0, 1]]
+    with pytest.raises(ValueError):
+        T.gradients_batched(1, x, y, models, stride=5)

@@ -1,79 +1,123 @@
-"""The torch restatement of the two TF1 CFA-GE graphs (off the reduction path):
-autograd gradients against central finite differences in float64, on CPU."""
+"""(f3) CFA-GE neighbour-gradient evaluation: the oracle's hand-derived gradients of the two TF1
+graphs (cfa_ge_2stage.py:391-433) pinned on the CPU by central finite differences (float64)
+and by an independent torch-autograd restatement of the same graphs; the HIP kernels
+(cfa_ge_grad_cnn_f32 / cfa_ge_grad_2nn_f32) are checked against the oracle in
+tests/test_gpu_grad.py."""
+import math
+
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
-from federated_amd.consensus import _tf1_models as M
+from oracle import cfa_oracle as orc
 
 
-def _fd_check(forward, params, x, y, idx_per_param=6, h=1e-6):
+# -- independent torch restatement of the TF1 graphs (test infrastructure only) ------------------
+def _same_pad(L, k, s):
+    out = math.ceil(L / s)
+    total = max((out - 1) * s + k - L, 0)
+    return total // 2, total - total // 2
+
+
+def _torch_cost(logits, y):
+    pred = torch.softmax(logits, dim=1)
+    return torch.mean(-torch.sum(y * torch.log(torch.clamp(pred, 1e-15, 0.99)), dim=1))
+
+
+def _torch_cnn(x, W1, b1, W2, b2, stride):
+    k = W1.shape[0]
+    pl, pr = _same_pad(x.shape[1], k, stride)
+    h = F.conv1d(F.pad(x.unsqueeze(1), (pl, pr)), W1.permute(2, 1, 0), b1, stride=stride)
+    h = torch.relu(h)
+    ql, qr = _same_pad(h.shape[2], stride, stride)
+    h = F.max_pool1d(F.pad(h, (ql, qr), value=float("-inf")), kernel_size=stride, stride=stride)
+    return h.permute(0, 2, 1).reshape(h.shape[0], -1) @ W2 + b2
+
+
+def _torch_2nn(x, W1, b1, W2, b2):
+    return torch.relu(x @ W1 + b1) @ W2 + b2
+
+
+def _torch_grads(fwd, params, x, y):
     ps = [torch.tensor(p, dtype=torch.float64, requires_grad=True) for p in params]
-    xx, yy = torch.tensor(x, dtype=torch.float64), torch.tensor(y, dtype=torch.float64)
-    loss = M._cost(forward(xx, *ps), yy)
-    grads = torch.autograd.grad(loss, ps)
-    rng = np.random.default_rng(0)
-    for p, g in zip(ps, grads):
-        flat = p.detach().reshape(-1)
-        for i in rng.choice(flat.numel(), size=min(idx_per_param, flat.numel()), replace=False):
-            def f(delta):
-                q = [t.detach().clone() for t in ps]
-                k = [j for j, t in enumerate(ps) if t is p][0]
-                q[k].reshape(-1)[i] += delta
-                return float(M._cost(forward(xx, *q), yy))
-            num = (f(h) - f(-h)) / (2 * h)
-            assert abs(num - float(g.reshape(-1)[i])) <= 1e-5 + 1e-4 * abs(num), (i, num, float(g.reshape(-1)[i]))
+    loss = _torch_cost(fwd(torch.tensor(x, dtype=torch.float64), *ps), torch.tensor(y, dtype=torch.float64))
+    return [g.numpy() for g in torch.autograd.grad(loss, ps)], float(loss)
 
 
-def test_cnn_gradients_finite_differences():
-    rng = np.random.default_rng(1)
-    # federated_sample_CNN_CFA-GE.py:36-42 shapes, small weights so softmax is not clipped
-    W1 = rng.standard_normal((16, 1, 8)) * 0.1
+def _cnn_case(rng, B=6, scale=0.3):
+    W1 = rng.standard_normal((16, 1, 8)) * scale
     b1 = rng.standard_normal(8) * 0.1
-    W2 = rng.standard_normal((168, 8)) * 0.05
-    b2 = rng.standard_normal(8) * 0.05
-    x = rng.standard_normal((4, 512))
-    y = np.eye(8)[[0, 3, 5, 7]]
-    _fd_check(lambda xx, *p: M.cnn_forward(xx, *p, stride=5), [W1, b1, W2, b2], x, y)
-    g = M.gradients(1, x, y, W1, b1, W2, b2, stride=5, device=torch.device("cpu"))
-    assert [a.shape for a in g] == [(16, 1, 8), (8,), (168, 8), (8,)]
+    W2 = rng.standard_normal((168, 8)) * 0.1
+    b2 = rng.standard_normal(8) * 0.1
+    x = rng.standard_normal((B, 512))
+    y = np.eye(8)[rng.integers(0, 8, B)]
+    return [W1, b1, W2, b2], x, y
 
 
-def test_2nn_gradients_finite_differences():
+def test_cnn_oracle_matches_autograd_and_finite_differences():
+    rng = np.random.default_rng(1)
+    params, x, y = _cnn_case(rng)
+    g, cost = orc.tf1_cnn_grads(x, y, *params, stride=5)
+    gt, cost_t = _torch_grads(lambda xx, *p: _torch_cnn(xx, *p, stride=5), params, x, y)
+    assert abs(cost - cost_t) < 1e-12
+    for a, b in zip(g, gt):
+        assert a.shape == b.shape and np.max(np.abs(a - b)) <= 1e-12 * max(1.0, np.max(np.abs(b)))
+    _fd(lambda p: orc.tf1_cnn_grads(x, y, *p, stride=5)[1], params, g)
+
+
+def test_2nn_oracle_matches_autograd_and_finite_differences():
     rng = np.random.default_rng(2)
-    W1, b1 = rng.standard_normal((64, 16)) * 0.2, rng.standard_normal(16) * 0.1
-    W2, b2 = rng.standard_normal((16, 8)) * 0.2, rng.standard_normal(8) * 0.1
+    params = [rng.standard_normal((64, 16)) * 0.2, rng.standard_normal(16) * 0.1,
+              rng.standard_normal((16, 8)) * 0.2, rng.standard_normal(8) * 0.1]
     x = rng.standard_normal((5, 64))
     y = np.eye(8)[[1, 2, 3, 4, 0]]
-    _fd_check(M.nn2_forward, [W1, b1, W2, b2], x, y)
+    g, cost = orc.tf1_2nn_grads(x, y, *params)
+    gt, cost_t = _torch_grads(_torch_2nn, params, x, y)
+    assert abs(cost - cost_t) < 1e-12
+    for a, b in zip(g, gt):
+        assert np.max(np.abs(a - b)) <= 1e-12 * max(1.0, np.max(np.abs(b)))
+    _fd(lambda p: orc.tf1_2nn_grads(x, y, *p)[1], params, g)
 
 
-def test_same_padding_shapes_match_tf_rule():
-    # FL_CFA_CNN_tf2/CFA-GE config: 512 inputs, stride 5 -> conv 103 -> pool 21 = multip
-    x = torch.zeros(2, 512)
-    out = M.cnn_forward(x, torch.zeros(16, 1, 8), torch.zeros(8), torch.zeros(168, 8), torch.zeros(8), stride=5)
-    assert out.shape == (2, 8)
-    assert M._same_pad(512, 16, 5) == (7, 7) and M._same_pad(103, 5, 5) == (1, 1)
+def _fd(cost_fn, params, grads, per_param=6, h=1e-6):
+    rng = np.random.default_rng(0)
+    for k, (p, g) in enumerate(zip(params, grads)):
+        for i in rng.choice(p.size, size=min(per_param, p.size), replace=False):
+            def f(delta):
+                q = [a.copy() for a in params]
+                q[k].reshape(-1)[i] += delta
+                return cost_fn(q)
+            num = (f(h) - f(-h)) / (2 * h)
+            assert abs(num - g.reshape(-1)[i]) <= 1e-6 + 1e-5 * abs(num), (k, i, num, g.reshape(-1)[i])
 
 
-@pytest.mark.parametrize("ml", [1, 2])
-def test_batched_gradients_match_per_model(ml):
-    """gradients_batched (all neighbour models in one vmapped forward/backward, f3) equals the
-    per-model evaluation within fp32 tolerance (1e-5 normwise per tensor)."""
-    import torch
-    from conftest import normwise_close
+def test_clip_saturation_blocks_the_gradient():
+    """Saturated softmax (pred > 0.99): tf.clip_by_value passes no gradient there."""
+    rng = np.random.default_rng(3)
+    params, x, y = _cnn_case(rng, B=4, scale=3.0)
+    params[3] = np.array([40.0, 0, 0, 0, 0, 0, 0, 0])  # class 0 saturates
+    y = np.eye(8)[[0, 0, 1, 0]]
+    g, _ = orc.tf1_cnn_grads(x, y, *params, stride=5)
+    gt, _ = _torch_grads(lambda xx, *p: _torch_cnn(xx, *p, stride=5), params, x, y)
+    for a, b in zip(g, gt):
+        assert np.allclose(a, b, rtol=1e-10, atol=1e-14)
+
+
+def test_same_padding_matches_tf_rule():
+    # CFA-GE config: 512 inputs, stride 5 -> conv 103 -> pool 21 = multip (federated_sample_CNN_CFA-GE.py:36-42)
+    assert _same_pad(512, 16, 5) == (7, 7) and _same_pad(103, 5, 5) == (1, 1)
+    logits, pooled, _, _ = orc.tf1_cnn_forward(np.zeros((2, 512)), np.zeros((16, 1, 8)), np.zeros(8),
+                                               np.zeros((168, 8)), np.zeros(8), 5)
+    assert logits.shape == (2, 8) and pooled.shape == (2, 21, 8)
+
+
+def test_product_gradients_need_the_gpu():
+    """No CPU fallback: without a GPU the f3 entry point raises."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
     from federated_amd.consensus import _tf1_models as M
-    rng = np.random.default_rng(ml)
-    if ml == 1:
-        shapes, xdim, stride = [(16, 1, 8), (8,), (168, 8), (8,)], 512, 5
-    else:
-        shapes, xdim, stride = [(64, 16), (16,), (16, 8), (8,)], 64, 1
-    models = [[(rng.standard_normal(s) * 0.1).astype(np.float32) for s in shapes] for _ in range(4)]
-    x = rng.standard_normal((6, xdim)).astype(np.float32)
-    y = np.eye(8, dtype=np.float32)[np.arange(6) % 8]
-    cpu = torch.device("cpu")
-    batched = M.gradients_batched(ml, x, y, models, stride=stride, device=cpu)
-    assert M.gradients_batched(ml, x, y, [], stride=stride, device=cpu) == []
-    for m, gb in zip(models, batched):
-        for a, r in zip(gb, M.gradients(ml, x, y, *m, stride=stride, device=cpu)):
-            assert a.shape == r.shape and normwise_close(a, r)
+    rng = np.random.default_rng(4)
+    params, x, y = _cnn_case(rng, B=2)
+    with pytest.raises(RuntimeError):
+        M.gradients(1, x, y, *params, stride=5)
