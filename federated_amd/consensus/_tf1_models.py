@@ -36,32 +36,62 @@ def _flat(model) -> np.ndarray:
 
 def gradients_batched(ml_model: int, x, y, models: Sequence, stride: int = 1, device=None) -> List[list]:
     """Gradients of the device's cost at every model of ``models`` (list of (W1, b1, W2, b2)),
-    in ONE kernel launch. Returns one list of four fp32 arrays per model."""
+    in ONE kernel launch. x, y and the models are packed into one pinned staging buffer (one
+    H2D); the gradients come back with one D2H. Returns one list of four fp32 arrays per model."""
     if not models:
         return []
-    eng = get_engine(device)
-    dev = eng.device
+    from ._runtime import mixer
+    hm = mixer() if device is None else None
+    eng = hm.engine if hm is not None else get_engine(device)
     W1 = np.asarray(models[0][0])
     shapes = [W1.shape, (int(np.size(models[0][1])),), np.asarray(models[0][2]).shape, (int(np.size(models[0][3])),)]
     sizes = [int(np.prod(s)) for s in shapes]
-    flat = np.stack([_flat(m) for m in models])
-    if flat.shape[1] != sum(sizes):
-        raise ValueError("all models must share the first model's shapes")
-    xt = torch.from_numpy(np.ascontiguousarray(np.asarray(x, np.float32))).to(dev)
-    yt = torch.from_numpy(np.ascontiguousarray(np.asarray(y, np.float32))).to(dev)
-    mt = torch.from_numpy(flat).to(dev)
-    gt = torch.empty_like(mt)
-    if ml_model == 1:
-        if W1.ndim != 3 or W1.shape[1] != 1:
-            raise ValueError("CNN W1 must be [filter, 1, number]")
-        eng.grad_cnn(xt, yt, mt, gt, filter=W1.shape[0], number=W1.shape[2], stride=int(stride))
-    elif ml_model == 2:
-        eng.grad_2nn(xt, yt, mt, gt, hidden=W1.shape[1])
+    P, M = sum(sizes), len(models)
+    x = np.asarray(x)
+    y = np.asarray(y)
+    if x.ndim != 2 or y.ndim != 2 or x.shape[0] != y.shape[0]:
+        raise ValueError("x must be [B, inputs] and y [B, classes]")
+    nx, ny = x.size, y.size
+    total = nx + ny + M * P
+    if hm is not None:
+        st = hm._stream()
+        host = hm._cached("h_grad", total, torch.float32, pinned=True)
+        dbuf = hm._cached("d_grad", total + M * P, torch.float32)
+        h_out = hm._cached("h_grad_out", M * P, torch.float32, pinned=True)
     else:
-        raise ValueError("Unable to set the ML model paramters")
-    g = gt.cpu().numpy()
+        st = torch.cuda.Stream(eng.device)
+        host = torch.empty(total, dtype=torch.float32, pin_memory=True)
+        dbuf = torch.empty(total + M * P, dtype=torch.float32, device=eng.device)
+        h_out = torch.empty(M * P, dtype=torch.float32, pin_memory=True)
+    hv = host.numpy()
+    hv[:nx] = x.reshape(-1)            # fp32 rounding, as the tf.float32 placeholders round
+    hv[nx:nx + ny] = y.reshape(-1)
+    mv = hv[nx + ny:].reshape(M, P)
     offs = np.concatenate([[0], np.cumsum(sizes)])
-    return [[g[i, offs[k]:offs[k + 1]].reshape(shapes[k]) for k in range(4)] for i in range(len(models))]
+    for i, m in enumerate(models):
+        parts = [np.asarray(m[0]), np.squeeze(m[1]), np.asarray(m[2]), np.squeeze(m[3])]
+        for k in range(4):
+            if np.size(parts[k]) != sizes[k]:
+                raise ValueError("all models must share the first model's shapes")
+            mv[i, offs[k]:offs[k + 1]] = np.asarray(parts[k]).reshape(-1)
+    with torch.cuda.stream(st):
+        dbuf[:total].copy_(host, non_blocking=True)
+        xt = dbuf[:nx].view(x.shape)
+        yt = dbuf[nx:nx + ny].view(y.shape)
+        mt = dbuf[nx + ny:total].view(M, P)
+        gt = dbuf[total:].view(M, P)
+        if ml_model == 1:
+            if W1.ndim != 3 or W1.shape[1] != 1:
+                raise ValueError("CNN W1 must be [filter, 1, number]")
+            eng.grad_cnn(xt, yt, mt, gt, filter=W1.shape[0], number=W1.shape[2], stride=int(stride), stream=st)
+        elif ml_model == 2:
+            eng.grad_2nn(xt, yt, mt, gt, hidden=W1.shape[1], stream=st)
+        else:
+            raise ValueError("Unable to set the ML model paramters")
+        h_out.copy_(dbuf[total:], non_blocking=True)
+        st.synchronize()
+        g = h_out.numpy().reshape(M, P).copy()
+    return [[g[i, offs[k]:offs[k + 1]].reshape(shapes[k]) for k in range(4)] for i in range(M)]
 
 
 def gradients(ml_model: int, x, y, W1, b1, W2, b2, stride: int = 1, device=None) -> list:

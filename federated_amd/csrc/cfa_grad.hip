@@ -23,6 +23,20 @@ namespace {
 
 constexpr float kClipLo = 1e-15f, kClipHi = 0.99f;
 
+// Phase timestamps for tools/probe/grad_phases.hip (compiled out of the library).
+#ifdef CFA_GRAD_PHASES
+__device__ unsigned long long g_phase[32];
+#define PHASE(k) \
+  do {           \
+    __syncthreads(); \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_phase[k] = wall_clock64(); \
+  } while (0)
+#else
+#define PHASE(k) \
+  do {           \
+  } while (0)
+#endif
+
 __host__ __device__ inline int same_left(int L, int k, int s) {
   const int out = (L + s - 1) / s;
   const int total = max((out - 1) * s + k - L, 0);
@@ -52,6 +66,25 @@ __device__ void softmax_xent_backward(float* z, const float* y, int C, float inv
   for (int c = 0; c < C; ++c) z[c] = (dpred(z[c], c) - dot) * z[c];
 }
 
+constexpr int kGradBlock = 512;  // 8 waves: these graphs are latency-bound, not ALU-bound
+
+// Copy n floats global -> LDS with every load of a thread issued before its first store (the
+// graphs are tiny, so serialized global latency, not bandwidth, would dominate).
+__device__ __forceinline__ void stage(float* dst, const float* src, int n, int tid, int T) {
+  constexpr int U = 8;
+  int i = tid;
+  for (; i + (U - 1) * T < n; i += U * T) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[i + u * T];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[i + u * T] = v[u];
+  }
+  for (; i < n; i += T) dst[i] = src[i];
+}
+
+constexpr int kMaxTaps = 32;  // conv filter taps held in registers (larger filters read LDS)
+
 struct CnnDims {
   int B, L, C, F, NC, S;
   int L1, L2, pl, ql;  // conv / pool output lengths, left pads
@@ -59,53 +92,112 @@ struct CnnDims {
   long long P;         // parameters per model
 };
 
-// Gradient sums run over all B samples; samples go through LDS in chunks of Bc. Each output
-// element is owned by one thread for the whole launch (the same index loop every chunk), so the
-// per-chunk partial sums accumulate in the output bucket without atomics, in a fixed order.
-__global__ __launch_bounds__(kBlock) void grad_cnn_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ y,
-                                                          const float* __restrict__ models,
-                                                          float* __restrict__ grads, CnnDims d) {
+// Per-sample LDS floats of the CNN kernel: x row, pooled / argmax / d pooled, logits, and the
+// per-sample partial sums of the conv-layer gradients.
+inline long long cnn_lds_per_sample(const CnnDims& d) {
+  const long long LN = (long long)d.L2 * d.NC;
+  return d.L + 3 * LN + 2LL * d.C + (long long)d.F * d.NC + d.NC;
+}
+inline long long cnn_lds_fixed(const CnnDims& d) {
+  const long long LN = (long long)d.L2 * d.NC;
+  return (long long)d.F * d.NC + d.NC + LN * d.C + d.C;
+}
+
+// Gradient sums run over all B samples; samples go through LDS in chunks of Bc. Every output
+// element is owned by one thread for the whole launch (the same index loop in every chunk), so
+// the per-chunk sums accumulate in the output bucket without atomics, in a fixed order.
+// FT, ST > 0: a filter of FT taps with stride (= pool size) ST at compile time: an interior
+// pooling window's (ST - 1) * ST + FT input samples are loaded once, all in flight together, and
+// its ST convolutions run from registers. FT = ST = 0: any geometry (runtime loops).
+template <int FT, int ST>
+__global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ y,
+                                                              const float* __restrict__ models,
+                                                              float* __restrict__ grads, CnnDims d) {
   extern __shared__ float lds[];
   const int LN = d.L2 * d.NC;
+  const int nW1 = d.F * d.NC, nW2 = LN * d.C, nG1 = nW1 + d.NC;
   float* W1 = lds;                        // [F][NC]
-  float* b1 = W1 + d.F * d.NC;            // [NC]
+  float* b1 = W1 + nW1;                   // [NC]
   float* W2 = b1 + d.NC;                  // [LN][C]
-  float* b2 = W2 + LN * d.C;              // [C]
-  float* pooled = b2 + d.C;               // [Bc][L2][NC]
+  float* b2 = W2 + nW2;                   // [C]
+  float* xs = b2 + d.C;                   // [Bc][L]
+  float* pooled = xs + d.Bc * d.L;        // [Bc][L2][NC]
   int* arg = reinterpret_cast<int*>(pooled + d.Bc * LN);  // conv position of each window's max
   float* dfc = reinterpret_cast<float*>(arg + d.Bc * LN); // [Bc][LN]
   float* zl = dfc + d.Bc * LN;            // [Bc][C]: logits, then d logits
+  float* ys = zl + d.Bc * d.C;            // [Bc][C] labels
+  float* part = ys + d.Bc * d.C;          // [Bc][nG1]: per-sample conv-gradient sums
   const float* m = models + (long long)blockIdx.x * d.P;
   float* g = grads + (long long)blockIdx.x * d.P;
   const int tid = threadIdx.x, T = blockDim.x;
-  const int nW1 = d.F * d.NC, nW2 = LN * d.C;
-  float* gW1 = g;
-  float* gb1 = gW1 + nW1;
-  float* gW2 = gb1 + d.NC;
+  float* gW2 = g + nG1;
   float* gb2 = gW2 + nW2;
   const float invB = 1.0f / (float)d.B;
 
-  for (int i = tid; i < nW1 + d.NC + nW2 + d.C; i += T) W1[i] = m[i];  // model bucket = W1 b1 W2 b2
+  PHASE(0);
+  stage(W1, m, nG1 + nW2 + d.C, tid, T);  // model bucket = W1 b1 W2 b2
   __syncthreads();
-
+  PHASE(1);
+  // the conv taps of this thread's channel stay in registers (T is a multiple of NC, so every
+  // item a thread takes below has the same channel c = tid % NC)
+  const bool taps_in_regs = d.F <= kMaxTaps && T % d.NC == 0;
+  float wreg[kMaxTaps];
+#pragma unroll
+  for (int k = 0; k < kMaxTaps; ++k) wreg[k] = (taps_in_regs && k < d.F) ? W1[k * d.NC + tid % d.NC] : 0.f;
   for (int b0 = 0; b0 < d.B; b0 += d.Bc) {
     const int nb = min(d.Bc, d.B - b0);
-    const float* xc = x + (long long)b0 * d.L;
-    const float* yc = y + (long long)b0 * d.C;
     const bool first = b0 == 0;
+    stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
+    stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
+    __syncthreads();
+    PHASE(2);
     // conv + bias + relu evaluated inside each pooling window; keep the max and its position
     for (int idx = tid; idx < nb * LN; idx += T) {
       const int b = idx / LN, r = idx % LN, q = r / d.NC, c = r % d.NC;
+      const float* xb = xs + b * d.L;
       float best = -INFINITY;
       int barg = -1;
-      for (int j = 0; j < d.S; ++j) {
+      bool done = false;
+      if constexpr (FT > 0 && ST > 0) {
+        // Every window, boundary ones included, takes this branch-free path: samples outside
+        // [0, L) read as 0 (a zero tap adds nothing: fma(0, w, z) == z) and positions outside
+        // [0, L1) never win, so no lane of a wave waits on a divergent slow path.
+        constexpr int NX = (ST - 1) * ST + FT;
+        const int p0 = q * ST - d.ql, t0 = p0 * ST - d.pl;
+        if (taps_in_regs) {
+          float xv[NX];
+#pragma unroll
+          for (int u = 0; u < NX; ++u) {
+            const int t = t0 + u;
+            const bool in = t >= 0 && t < d.L;
+            const float v = xb[in ? t : 0];
+            xv[u] = in ? v : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < ST; ++j) {
+            float z = 0.f;
+#pragma unroll
+            for (int k = 0; k < FT; ++k) z = fmaf(xv[j * ST + k], wreg[k], z);
+            z += b1[c];
+            const float h = z > 0.f ? z : 0.f;
+            const int p = p0 + j;
+            if (p >= 0 && p < d.L1 && h > best) {
+              best = h;
+              barg = p;
+            }
+          }
+          done = true;
+        }
+      }
+      for (int j = 0; j < d.S && !done; ++j) {
         const int p = q * d.S - d.ql + j;
         if (p < 0 || p >= d.L1) continue;
+        const int t0 = p * d.S - d.pl;
         float z = 0.f;
         for (int k = 0; k < d.F; ++k) {
-          const int t = p * d.S + k - d.pl;
-          if (t >= 0 && t < d.L) z = fmaf(xc[b * d.L + t], W1[k * d.NC + c], z);
+          const int t = t0 + k;
+          if (t >= 0 && t < d.L) z = fmaf(xb[t], W1[k * d.NC + c], z);
         }
         z += b1[c];
         const float h = z > 0.f ? z : 0.f;
@@ -118,20 +210,29 @@ __global__ __launch_bounds__(kBlock) void grad_cnn_kernel(const float* __restric
       arg[idx] = barg;
     }
     __syncthreads();
-    for (int idx = tid; idx < nb * d.C; idx += T) {  // logits
-      const int b = idx / d.C, k = idx % d.C;
+    PHASE(3);
+    // logits: 8 lanes per (sample, class), strided partial sums, xor-shuffle reduction
+    for (int idx = tid; idx < nb * d.C * 8; idx += T) {
+      const int o = idx >> 3, lane = idx & 7;
+      const int b = o / d.C, k = o % d.C;
       float z = 0.f;
-      for (int i = 0; i < LN; ++i) z = fmaf(pooled[b * LN + i], W2[i * d.C + k], z);
-      zl[idx] = z + b2[k];
+      for (int i = lane; i < LN; i += 8) z = fmaf(pooled[b * LN + i], W2[i * d.C + k], z);
+      z += __shfl_xor(z, 1, 8);
+      z += __shfl_xor(z, 2, 8);
+      z += __shfl_xor(z, 4, 8);
+      if (lane == 0) zl[o] = z + b2[k];
     }
     __syncthreads();
-    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, yc + b * d.C, d.C, invB);
+    PHASE(4);
+    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, ys + b * d.C, d.C, invB);
     __syncthreads();
+    PHASE(5);
 
     // dense layer gradients and the gradient flowing into the pooled features
     for (int idx = tid; idx < nW2; idx += T) {
       const int i = idx / d.C, k = idx % d.C;
       float s = first ? 0.f : gW2[idx];
+#pragma unroll 8
       for (int b = 0; b < nb; ++b) s = fmaf(pooled[b * LN + i], zl[b * d.C + k], s);
       gW2[idx] = s;
     }
@@ -147,52 +248,69 @@ __global__ __launch_bounds__(kBlock) void grad_cnn_kernel(const float* __restric
       dfc[idx] = pooled[idx] > 0.f ? s : 0.f;  // relu gradient at the window's max
     }
     __syncthreads();
-
-    // conv gradients: only each window's max position receives gradient (windows do not overlap)
-    for (int idx = tid; idx < nW1 + d.NC; idx += T) {
-      if (idx < nW1) {
-        const int k = idx / d.NC, c = idx % d.NC;
-        float s = first ? 0.f : gW1[idx];
-        for (int b = 0; b < nb; ++b)
-          for (int q = 0; q < d.L2; ++q) {
-            const int e = b * LN + q * d.NC + c;
-            const float gz = dfc[e];
-            const int t = arg[e] * d.S + k - d.pl;
-            if (gz != 0.f && t >= 0 && t < d.L) s = fmaf(gz, xc[b * d.L + t], s);
-          }
-        gW1[idx] = s;
+    PHASE(6);
+    // conv gradients per (weight, sample): only each window's max position receives gradient
+    for (int idx = tid; idx < nG1 * nb; idx += T) {  // e fastest: lanes read neighbouring channels
+      const int e = idx % nG1, b = idx / nG1;
+      float s = 0.f;
+      if (e < nW1) {
+        const int k = e / d.NC, c = e % d.NC;
+#pragma unroll 7
+        for (int q = 0; q < d.L2; ++q) {  // select, not branch: the loads stay in flight together
+          const int f = b * LN + q * d.NC + c;
+          const int t = arg[f] * d.S + k - d.pl;
+          const bool in = t >= 0 && t < d.L;
+          const float xv = xs[b * d.L + (in ? t : 0)];
+          s = fmaf(dfc[f], in ? xv : 0.f, s);
+        }
       } else {
-        const int c = idx - nW1;
-        float s = first ? 0.f : gb1[c];
-        for (int b = 0; b < nb; ++b)
-          for (int q = 0; q < d.L2; ++q) s += dfc[b * LN + q * d.NC + c];
-        gb1[c] = s;
+        const int c = e - nW1;
+#pragma unroll 7
+        for (int q = 0; q < d.L2; ++q) s += dfc[b * LN + q * d.NC + c];
       }
+      part[b * nG1 + e] = s;
+    }
+    __syncthreads();
+    PHASE(7);
+    for (int e = tid; e < nG1; e += T) {  // sum over the chunk's samples in order
+      float s = first ? 0.f : g[e];
+      for (int b = 0; b < nb; ++b) s += part[b * nG1 + e];
+      g[e] = s;
     }
     __syncthreads();  // the chunk's LDS is reused by the next one
+    PHASE(8);
   }
 }
 
+constexpr int kSpan = 32;  // first-layer inputs per partial sum (W1 slice held in registers)
+
 struct NnDims {
   int B, L, H, C;
+  int G;   // ceil(L / kSpan) slices of the input dimension for the first layer's partial sums
   int Bc;
   long long P;
 };
 
-__global__ __launch_bounds__(kBlock) void grad_2nn_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ y,
-                                                          const float* __restrict__ models,
-                                                          float* __restrict__ grads, NnDims d) {
+inline long long nn_lds_per_sample(const NnDims& d) { return d.L + 2LL * d.H + 2LL * d.C + (long long)d.G * d.H; }
+inline long long nn_lds_fixed(const NnDims& d) { return d.H + (long long)d.H * d.C + d.C; }
+
+__global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ y,
+                                                              const float* __restrict__ models,
+                                                              float* __restrict__ grads, NnDims d) {
   extern __shared__ float lds[];
   float* b1 = lds;                 // [H]
   float* W2 = b1 + d.H;            // [H][C]
   float* b2 = W2 + d.H * d.C;      // [C]
-  float* act = b2 + d.C;           // [Bc][H] relu(x W1 + b1)
+  float* xs = b2 + d.C;            // [Bc][L]
+  float* act = xs + d.Bc * d.L;    // [Bc][H] relu(x W1 + b1)
   float* dz = act + d.Bc * d.H;    // [Bc][H]
   float* zl = dz + d.Bc * d.H;     // [Bc][C]
+  float* ys = zl + d.Bc * d.C;     // [Bc][C]
+  float* zpart = ys + d.Bc * d.C;  // [G][Bc][H]
   const long long nW1 = (long long)d.L * d.H;
   const float* m = models + (long long)blockIdx.x * d.P;
-  const float* W1 = m;             // [L][H], read from global (L2-resident)
+  const float* W1 = m;             // [L][H], read from global once per launch (kept in registers)
   float* g = grads + (long long)blockIdx.x * d.P;
   float* gW1 = g;
   float* gb1 = gW1 + nW1;
@@ -200,22 +318,68 @@ __global__ __launch_bounds__(kBlock) void grad_2nn_kernel(const float* __restric
   float* gb2 = gW2 + d.H * d.C;
   const int tid = threadIdx.x, T = blockDim.x;
   const float invB = 1.0f / (float)d.B;
+  const int H4 = (d.H % 4 == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0) ? d.H / 4 : 0;
 
-  for (int i = tid; i < d.H + d.H * d.C + d.C; i += T) b1[i] = m[nW1 + i];
-  __syncthreads();
+  PHASE(10);
+  stage(b1, m + nW1, d.H + d.H * d.C + d.C, tid, T);
+  // W1 slice of this thread's (slice, h) pairs: with G * H <= T every thread owns one pair and
+  // loads its kSpan weights once, all in flight together
+  const bool w_in_regs = d.G * d.H <= T;
+  float wreg[kSpan];
+  {
+    const int h = tid % d.H, grp = tid / d.H, i0 = grp * kSpan;
+#pragma unroll
+    for (int u = 0; u < kSpan; ++u)
+      wreg[u] = (w_in_regs && grp < d.G && i0 + u < d.L) ? W1[(long long)(i0 + u) * d.H + h] : 0.f;
+  }
   for (int b0 = 0; b0 < d.B; b0 += d.Bc) {
     const int nb = min(d.Bc, d.B - b0);
-    const float* xc = x + (long long)b0 * d.L;
-    const float* yc = y + (long long)b0 * d.C;
     const bool first = b0 == 0;
+    stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
+    stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
+    __syncthreads();
+    PHASE(11);
+    // first layer as G partial sums over kSpan-wide slices of the input dimension
+    if (w_in_regs) {
+      const int h = tid % d.H, grp = tid / d.H, i0 = grp * kSpan;
+      if (grp < d.G) {
+        for (int b = 0; b < nb; ++b) {
+          const float* xb = xs + b * d.L + i0;
+          float z = 0.f;
+          if (i0 + kSpan <= d.L) {  // full slice: every load issued before the FMA chain
+            float xv[kSpan];
+#pragma unroll
+            for (int u = 0; u < kSpan; ++u) xv[u] = xb[u];
+#pragma unroll
+            for (int u = 0; u < kSpan; ++u) z = fmaf(xv[u], wreg[u], z);
+          } else {
+#pragma unroll
+            for (int u = 0; u < kSpan; ++u)
+              if (u < d.L - i0) z = fmaf(xb[u], wreg[u], z);
+          }
+          zpart[(grp * d.Bc + b) * d.H + h] = z;
+        }
+      }
+    } else {
+      for (int idx = tid; idx < d.G * nb * d.H; idx += T) {
+        const int h = idx % d.H, r = idx / d.H, b = r % nb, grp = r / nb;
+        const int i0 = grp * kSpan, i1 = min(d.L, i0 + kSpan);
+        float z = 0.f;
+        for (int i = i0; i < i1; ++i) z = fmaf(xs[b * d.L + i], W1[(long long)i * d.H + h], z);
+        zpart[(grp * d.Bc + b) * d.H + h] = z;
+      }
+    }
+    __syncthreads();
+    PHASE(12);
     for (int idx = tid; idx < nb * d.H; idx += T) {
       const int b = idx / d.H, h = idx % d.H;
       float z = 0.f;
-      for (int i = 0; i < d.L; ++i) z = fmaf(xc[b * d.L + i], W1[(long long)i * d.H + h], z);
+      for (int grp = 0; grp < d.G; ++grp) z += zpart[(grp * d.Bc + b) * d.H + h];
       z += b1[h];
       act[idx] = z > 0.f ? z : 0.f;
     }
     __syncthreads();
+    PHASE(13);
     for (int idx = tid; idx < nb * d.C; idx += T) {
       const int b = idx / d.C, k = idx % d.C;
       float z = 0.f;
@@ -223,8 +387,10 @@ __global__ __launch_bounds__(kBlock) void grad_2nn_kernel(const float* __restric
       zl[idx] = z + b2[k];
     }
     __syncthreads();
-    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, yc + b * d.C, d.C, invB);
+    PHASE(14);
+    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, ys + b * d.C, d.C, invB);
     __syncthreads();
+    PHASE(15);
     for (int idx = tid; idx < d.H * d.C; idx += T) {
       const int h = idx / d.C, k = idx % d.C;
       float s = first ? 0.f : gW2[idx];
@@ -243,11 +409,40 @@ __global__ __launch_bounds__(kBlock) void grad_2nn_kernel(const float* __restric
       dz[idx] = act[idx] > 0.f ? s : 0.f;
     }
     __syncthreads();
-    for (long long idx = tid; idx < nW1; idx += T) {  // consecutive lanes: consecutive h (coalesced)
-      const int i = (int)(idx / d.H), h = (int)(idx % d.H);
-      float s = first ? 0.f : gW1[idx];
-      for (int b = 0; b < nb; ++b) s = fmaf(xc[b * d.L + i], dz[b * d.H + h], s);
-      gW1[idx] = s;
+    PHASE(16);
+    if (H4) {  // gW1 = x^T dz, four h per thread: one x read feeds four FMAs
+      const f4* dz4 = reinterpret_cast<const f4*>(dz);
+      f4* gW14 = reinterpret_cast<f4*>(gW1);
+      const bool aligned = (reinterpret_cast<uintptr_t>(gW1) & 15) == 0;
+      for (long long idx = tid; idx < nW1 / 4; idx += T) {
+        const int i = (int)(idx / H4), hq = (int)(idx % H4);
+        f4 s;
+        if (first) {
+          s = f4{0.f, 0.f, 0.f, 0.f};
+        } else if (aligned) {
+          s = gW14[idx];
+        } else {
+          for (int c = 0; c < 4; ++c) s[c] = gW1[idx * 4 + c];
+        }
+#pragma unroll 8
+        for (int b = 0; b < nb; ++b) {
+          const float xv = xs[b * d.L + i];
+          const f4 dv = dz4[b * H4 + hq];
+          s.x = fmaf(xv, dv.x, s.x);
+          s.y = fmaf(xv, dv.y, s.y);
+          s.z = fmaf(xv, dv.z, s.z);
+          s.w = fmaf(xv, dv.w, s.w);
+        }
+        if (aligned) gW14[idx] = s;
+        else for (int c = 0; c < 4; ++c) gW1[idx * 4 + c] = s[c];
+      }
+    } else {
+      for (long long idx = tid; idx < nW1; idx += T) {
+        const int i = (int)(idx / d.H), h = (int)(idx % d.H);
+        float s = first ? 0.f : gW1[idx];
+        for (int b = 0; b < nb; ++b) s = fmaf(xs[b * d.L + i], dz[b * d.H + h], s);
+        gW1[idx] = s;
+      }
     }
     for (int h = tid; h < d.H; h += T) {
       float s = first ? 0.f : gb1[h];
@@ -255,17 +450,33 @@ __global__ __launch_bounds__(kBlock) void grad_2nn_kernel(const float* __restric
       gb1[h] = s;
     }
     __syncthreads();
+    PHASE(17);
   }
 }
 
-// Dynamic LDS per workgroup: the device limit, capped at 64 KiB (the default dynamic-LDS bound of
-// a kernel without a raised attribute); larger sample counts run in chunks.
-int lds_limit() {
+// Dynamic LDS for one workgroup: up to 64 KiB by default; above that the kernel's limit is
+// raised to the device's (160 KiB on gfx950) when the runtime allows it.
+int device_lds_max() {
   int dev = 0, v = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 65536;
   if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0)
     return 65536;
-  return std::min(v, 65536);
+  return v;
+}
+
+// Samples per chunk for `fixed` + Bc * `per_sample` floats of LDS; sets *bytes. 0 if not even one fits.
+int plan_chunk(const void* kernel, long long fixed, long long per_sample, int B, long long* bytes) {
+  long long limit = device_lds_max();
+  if (const char* cap = getenv("CFA_GRAD_LDS_CAP")) limit = std::min<long long>(limit, atoll(cap));  // measurement knob
+  auto fit = [&](long long lim) { return (int)std::min<long long>(B, (lim / 4 - fixed) / per_sample); };
+  int bc = fit(limit);
+  if (4 * (fixed + per_sample * bc) > 65536 &&
+      hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)limit) != hipSuccess) {
+    (void)hipGetLastError();
+    bc = fit(65536);
+  }
+  *bytes = 4 * (fixed + per_sample * std::max(bc, 0));
+  return std::max(bc, 0);
 }
 
 }  // namespace
@@ -284,16 +495,19 @@ extern "C" int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L,
   d.L2 = (d.L1 + stride - 1) / stride;
   d.pl = same_left(L, filter, stride);
   d.ql = same_left(d.L1, stride, stride);
-  const long long LN = (long long)d.L2 * number;
-  d.P = (long long)filter * number + number + LN * classes + classes;
-  const long long fixed = 4LL * (d.F * d.NC + d.NC + LN * d.C + d.C);
-  const long long per_sample = 4LL * (3LL * LN + d.C);
-  const long long room = (long long)lds_limit() - fixed;
-  if (room < per_sample)
-    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_cnn_f32: the model alone needs %lld bytes of LDS", fixed);
-  d.Bc = (int)std::min<long long>(B, room / per_sample);
-  const long long lds = fixed + per_sample * d.Bc;
-  grad_cnn_kernel<<<M, kBlock, (size_t)lds, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+  d.P = (long long)filter * number + number + (long long)d.L2 * number * classes + classes;
+  long long bytes = 0;
+  // the CFA-GE CNN's geometry (filter 16, stride 5: federated_sample_CNN_CFA-GE.py:36-39) gets
+  // the unrolled kernel
+  const bool fast = filter == 16 && stride == 5;
+  const void* kern = fast ? (const void*)grad_cnn_kernel<16, 5> : (const void*)grad_cnn_kernel<0, 0>;
+  d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), B, &bytes);
+  if (d.Bc < 1)
+    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_cnn_f32: one sample does not fit the workgroup's LDS");
+  if (fast)
+    grad_cnn_kernel<16, 5><<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+  else
+    grad_cnn_kernel<0, 0><<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
   return check_launch("grad_cnn_kernel");
 }
 
@@ -307,14 +521,12 @@ extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L,
   if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "cfa_ge_grad_2nn_f32: null buffer");
   NnDims d;
   d.B = B, d.L = L, d.H = hidden, d.C = classes;
+  d.G = (L + kSpan - 1) / kSpan;
   d.P = (long long)L * hidden + hidden + (long long)hidden * classes + classes;
-  const long long fixed = 4LL * (hidden + (long long)hidden * classes + classes);
-  const long long per_sample = 4LL * (2LL * hidden + classes);
-  const long long room = (long long)lds_limit() - fixed;
-  if (room < per_sample)
-    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_2nn_f32: the model alone needs %lld bytes of LDS", fixed);
-  d.Bc = (int)std::min<long long>(B, room / per_sample);
-  const long long lds = fixed + per_sample * d.Bc;
-  grad_2nn_kernel<<<M, kBlock, (size_t)lds, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+  long long bytes = 0;
+  d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), B, &bytes);
+  if (d.Bc < 1)
+    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_2nn_f32: one sample does not fit the workgroup's LDS");
+  grad_2nn_kernel<<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
   return check_launch("grad_2nn_kernel");
 }
