@@ -11,8 +11,13 @@ from conftest import ROOT
 HEADER = os.path.join(ROOT, "include", "cfa_engine.h")
 
 
+def _header_text():
+    with open(HEADER) as fh:
+        return fh.read()
+
+
 def header_symbols():
-    text = open(HEADER).read()
+    text = _header_text()
     return sorted(set(re.findall(r"CFA_API\s+[\w\s\*]+?\b(cfa_\w+)\s*\(", text)))
 
 
@@ -40,7 +45,7 @@ def test_library_exports_every_header_symbol():
 def test_ctypes_table_matches_header():
     from federated_amd import _lib
     assert sorted(_lib.SIGNATURES) == header_symbols()
-    text = open(HEADER).read()
+    text = _header_text()
     for name, (_, args) in _lib.SIGNATURES.items():
         m = re.search(r"\b%s\s*\(([^)]*)\)" % name, text, re.S)
         decl = m.group(1).strip()

@@ -42,7 +42,7 @@ def _torch_2nn(x, W1, b1, W2, b2):
 def _torch_grads(fwd, params, x, y):
     ps = [torch.tensor(p, dtype=torch.float64, requires_grad=True) for p in params]
     loss = _torch_cost(fwd(torch.tensor(x, dtype=torch.float64), *ps), torch.tensor(y, dtype=torch.float64))
-    return [g.numpy() for g in torch.autograd.grad(loss, ps)], float(loss)
+    return [g.numpy() for g in torch.autograd.grad(loss, ps)], float(loss.detach())
 
 
 def _cnn_case(rng, B=6, scale=0.3):
