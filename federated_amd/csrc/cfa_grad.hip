@@ -113,6 +113,8 @@ template <int FT, int ST>
 __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ y,
                                                               const float* __restrict__ models,
+                                                              const int* __restrict__ mrow,
+                                                              const int* __restrict__ drow,
                                                               float* __restrict__ grads, CnnDims d) {
   extern __shared__ float lds[];
   const int LN = d.L2 * d.NC;
@@ -128,7 +130,12 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   float* zl = dfc + d.Bc * LN;            // [Bc][C]: logits, then d logits
   float* ys = zl + d.Bc * d.C;            // [Bc][C] labels
   float* part = ys + d.Bc * d.C;          // [Bc][nG1]: per-sample conv-gradient sums
-  const float* m = models + (long long)blockIdx.x * d.P;
+  // model and data rows of this workgroup's evaluation (population form), else model blockIdx.x
+  // on the one data set
+  const float* m = models + (long long)(mrow ? mrow[blockIdx.x] : (int)blockIdx.x) * d.P;
+  const long long dr = drow ? drow[blockIdx.x] : 0;
+  x += dr * d.B * d.L;
+  y += dr * d.B * d.C;
   float* g = grads + (long long)blockIdx.x * d.P;
   const int tid = threadIdx.x, T = blockDim.x;
   float* gW2 = g + nG1;
@@ -297,6 +304,8 @@ inline long long nn_lds_fixed(const NnDims& d) { return d.H + (long long)d.H * d
 __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ y,
                                                               const float* __restrict__ models,
+                                                              const int* __restrict__ mrow,
+                                                              const int* __restrict__ drow,
                                                               float* __restrict__ grads, NnDims d) {
   extern __shared__ float lds[];
   float* b1 = lds;                 // [H]
@@ -309,7 +318,10 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
   float* ys = zl + d.Bc * d.C;     // [Bc][C]
   float* zpart = ys + d.Bc * d.C;  // [G][Bc][H]
   const long long nW1 = (long long)d.L * d.H;
-  const float* m = models + (long long)blockIdx.x * d.P;
+  const float* m = models + (long long)(mrow ? mrow[blockIdx.x] : (int)blockIdx.x) * d.P;
+  const long long dr = drow ? drow[blockIdx.x] : 0;
+  x += dr * d.B * d.L;
+  y += dr * d.B * d.C;
   const float* W1 = m;             // [L][H], read from global once per launch (kept in registers)
   float* g = grads + (long long)blockIdx.x * d.P;
   float* gW1 = g;
@@ -481,14 +493,16 @@ int plan_chunk(const void* kernel, long long fixed, long long per_sample, int B,
 
 }  // namespace
 
-extern "C" int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L, int classes,
-                                   int filter, int number, int stride, const float* models,
-                                   float* grads, int M, void* stream) {
+namespace {
+
+int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L, int classes, int filter,
+                    int number, int stride, const float* models, const int* mrow, const int* drow,
+                    float* grads, int M, void* stream) {
   if (M < 0 || B < 1 || L < 1 || classes < 1 || filter < 1 || number < 1 || stride < 1)
-    return fail(CFA_E_INVALID, "cfa_ge_grad_cnn_f32: bad dimensions (B %d L %d C %d F %d NC %d S %d M %d)",
-                B, L, classes, filter, number, stride, M);
+    return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d C %d F %d NC %d S %d M %d)", fn, B, L, classes,
+                filter, number, stride, M);
   if (M == 0) return CFA_OK;
-  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "cfa_ge_grad_cnn_f32: null buffer");
+  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   CnnDims d;
   d.B = B, d.L = L, d.C = classes, d.F = filter, d.NC = number, d.S = stride;
   d.L1 = (L + stride - 1) / stride;
@@ -502,31 +516,64 @@ extern "C" int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L,
   const bool fast = filter == 16 && stride == 5;
   const void* kern = fast ? (const void*)grad_cnn_kernel<16, 5> : (const void*)grad_cnn_kernel<0, 0>;
   d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), B, &bytes);
-  if (d.Bc < 1)
-    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_cnn_f32: one sample does not fit the workgroup's LDS");
+  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
+  hipStream_t st = static_cast<hipStream_t>(stream);
   if (fast)
-    grad_cnn_kernel<16, 5><<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+    grad_cnn_kernel<16, 5><<<M, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, grads, d);
   else
-    grad_cnn_kernel<0, 0><<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+    grad_cnn_kernel<0, 0><<<M, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, grads, d);
   return check_launch("grad_cnn_kernel");
 }
 
-extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, int hidden,
-                                   int classes, const float* models, float* grads, int M,
-                                   void* stream) {
+int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L, int hidden, int classes,
+                    const float* models, const int* mrow, const int* drow, float* grads, int M, void* stream) {
   if (M < 0 || B < 1 || L < 1 || hidden < 1 || classes < 1)
-    return fail(CFA_E_INVALID, "cfa_ge_grad_2nn_f32: bad dimensions (B %d L %d H %d C %d M %d)", B, L, hidden,
-                classes, M);
+    return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d H %d C %d M %d)", fn, B, L, hidden, classes, M);
   if (M == 0) return CFA_OK;
-  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "cfa_ge_grad_2nn_f32: null buffer");
+  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   NnDims d;
   d.B = B, d.L = L, d.H = hidden, d.C = classes;
   d.G = (L + kSpan - 1) / kSpan;
   d.P = (long long)L * hidden + hidden + (long long)hidden * classes + classes;
   long long bytes = 0;
   d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), B, &bytes);
-  if (d.Bc < 1)
-    return fail(CFA_E_UNSUPPORTED, "cfa_ge_grad_2nn_f32: one sample does not fit the workgroup's LDS");
-  grad_2nn_kernel<<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, grads, d);
+  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
+  grad_2nn_kernel<<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, mrow, drow,
+                                                                                     grads, d);
   return check_launch("grad_2nn_kernel");
+}
+
+}  // namespace
+
+extern "C" int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L, int classes,
+                                   int filter, int number, int stride, const float* models,
+                                   float* grads, int M, void* stream) {
+  return launch_grad_cnn("cfa_ge_grad_cnn_f32", x, y, B, L, classes, filter, number, stride, models, nullptr,
+                         nullptr, grads, M, stream);
+}
+
+extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, int hidden,
+                                   int classes, const float* models, float* grads, int M,
+                                   void* stream) {
+  return launch_grad_2nn("cfa_ge_grad_2nn_f32", x, y, B, L, hidden, classes, models, nullptr, nullptr, grads, M,
+                         stream);
+}
+
+extern "C" int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,
+                                        int filter, int number, int stride, const float* models,
+                                        const int32_t* model_row, const int32_t* data_row,
+                                        float* grads, int M, void* stream) {
+  if (M > 0 && (!model_row || !data_row))
+    return fail(CFA_E_INVALID, "cfa_ge_grad_cnn_rows_f32: null row table");
+  return launch_grad_cnn("cfa_ge_grad_cnn_rows_f32", x, y, B, L, classes, filter, number, stride, models,
+                         model_row, data_row, grads, M, stream);
+}
+
+extern "C" int cfa_ge_grad_2nn_rows_f32(const float* x, const float* y, int B, int L, int hidden,
+                                        int classes, const float* models, const int32_t* model_row,
+                                        const int32_t* data_row, float* grads, int M, void* stream) {
+  if (M > 0 && (!model_row || !data_row))
+    return fail(CFA_E_INVALID, "cfa_ge_grad_2nn_rows_f32: null row table");
+  return launch_grad_2nn("cfa_ge_grad_2nn_rows_f32", x, y, B, L, hidden, classes, models, model_row, data_row,
+                         grads, M, stream);
 }

@@ -306,3 +306,99 @@ extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const
   return CFA_OK;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// CFA-GE population step (cfa_ge_population_step_f32): stage-1 mix and the neighbours' gradient
+// step of every device in one launch (cfa_ge_2stage.py:446-466 then :591-621). The operations
+// and their order are those of cfa_mix_population_f32 followed by cfa_mewma_update_f32, so the
+// result is identical to the two launches, minus one write and one read of every mixed model.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct GeStepArgs {
+  float* const* out;
+  const float* const* src;
+  float* const* state;
+  const float* const* grad;
+  const int32_t* ptr;
+  const int32_t* idx;
+  const float* coef;
+  float rho, one_minus_rho, lr1, lr2;
+  long long split;
+  int filtered;
+};
+
+__device__ __forceinline__ float ge_lr(const GeStepArgs& a, long long i) { return i < a.split ? a.lr1 : a.lr2; }
+
+__global__ __launch_bounds__(kBlock) void ge_step_kernel(GeStepArgs a, long long nvec, long long P) {
+  const int d = blockIdx.y;
+  const int e0 = a.ptr[d], e1 = a.ptr[d + 1];
+  float* out = a.out[d];
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
+    f4 w = ld4<false>(a.src[a.idx[e0]], i);
+    for (int e = e0 + 1; e < e1; ++e) {  // stage 1: sequential rule
+      const f4 x = ld4<false>(a.src[a.idx[e]], i);
+      f4 t = x - w;
+      t = a.coef[e] * t;
+      w = w + t;
+    }
+    f4 lr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lr[c] = ge_lr(a, i * 4 + c);
+    for (int e = e0 + 1; e < e1; ++e) {  // gradient step: MEWMA filter + SGD
+      const float* gp = a.grad[e];
+      const f4 g = gp ? ld4<false>(gp, i) : f4{0.f, 0.f, 0.f, 0.f};
+      const f4 s_old = ld4<false>(a.state[e], i);
+      const f4 s = a.rho * g + a.one_minus_rho * s_old;
+      st4<false>(a.state[e], i, s);
+      w = w - lr * (a.filtered ? s : g);
+    }
+    st4<false>(out, i, w);
+  }
+  if (blockIdx.x == 0) {  // the < 4-element tail
+    for (long long i = nvec * 4 + threadIdx.x; i < P; i += kBlock) {
+      float w = a.src[a.idx[e0]][i];
+      for (int e = e0 + 1; e < e1; ++e) {
+        float t = a.src[a.idx[e]][i] - w;
+        t = a.coef[e] * t;
+        w = w + t;
+      }
+      const float lr = ge_lr(a, i);
+      for (int e = e0 + 1; e < e1; ++e) {
+        const float g = a.grad[e] ? a.grad[e][i] : 0.f;
+        const float t1 = a.rho * g;
+        const float t2 = a.one_minus_rho * a.state[e][i];
+        const float s = t1 + t2;
+        a.state[e][i] = s;
+        w = w - lr * (a.filtered ? s : g);
+      }
+      out[i] = w;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int cfa_ge_population_step_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                          float* const* state_ptrs, const float* const* grad_ptrs,
+                                          const int32_t* csr_ptr, const int32_t* csr_idx,
+                                          const float* csr_coef, int D, double rho, float lr1,
+                                          float lr2, size_t lr_split, int use_filtered, size_t P,
+                                          void* stream) {
+  if (D < 0) return fail(CFA_E_INVALID, "negative device count");
+  if (D == 0 || P == 0) return CFA_OK;
+  if (!out_ptrs || !src_ptrs || !state_ptrs || !grad_ptrs || !csr_ptr || !csr_idx || !csr_coef)
+    return fail(CFA_E_INVALID, "null population table");
+  if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
+  GeStepArgs a{out_ptrs, src_ptrs, state_ptrs, grad_ptrs, csr_ptr, csr_idx, csr_coef,
+               (float)rho, (float)(1.0 - rho), lr1, lr2, (long long)lr_split, use_filtered ? 1 : 0};
+  // buckets are 16-byte aligned (allocator contract, checked by the host layer)
+  const long long nvec = (long long)P / 4;
+  long long gx = (nvec + kBlock - 1) / kBlock;
+  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  dim3 grid((unsigned)gx, (unsigned)D);
+  ge_step_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(a, nvec, (long long)P);
+  return check_launch("ge_step_kernel");
+}

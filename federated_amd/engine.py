@@ -345,6 +345,41 @@ class Engine:
                   grads.data_ptr(), M, self.stream_handle(stream))
         return grads
 
+    def grad_rows(self, ml_model: int, x: torch.Tensor, y: torch.Tensor, models: torch.Tensor,
+                  model_row: torch.Tensor, data_row: torch.Tensor, grads: torch.Tensor, geom: dict,
+                  stream=None) -> torch.Tensor:
+        """Population form (cfa_ge_grad_{cnn,2nn}_rows_f32): evaluation m = gradient of data row
+        data_row[m] (x [Dx, B, L], y [Dx, B, C]) at model row model_row[m] of models [Dm, P],
+        into grads [M, P]. ``geom``: filter/number/stride (CNN) or intermediate_nodes (2NN)."""
+        for name, t, nd in (("x", x, 3), ("y", y, 3)):
+            if not t.is_cuda or t.dtype != torch.float32 or t.dim() != nd or not t.is_contiguous():
+                raise TypeError(f"{name} must be a contiguous 3-D fp32 CUDA tensor")
+        Dm, P = _check_2d(models, "models")
+        M, Pg = _check_2d(grads, "grads")
+        for name, t in (("model_row", model_row), ("data_row", data_row)):
+            if not t.is_cuda or t.dtype != torch.int32 or t.numel() != M or not t.is_contiguous():
+                raise TypeError(f"{name} must be a contiguous int32 CUDA tensor of {M} entries")
+        Dx, B, L = (int(v) for v in x.shape)
+        if tuple(y.shape[:2]) != (Dx, B) or Pg != P:
+            raise ValueError("y must be [Dx, B, C] and grads [M, P]")
+        C = int(y.shape[2])
+        if ml_model == 1:
+            F, NC, S = int(geom["filter"]), int(geom["number"]), int(geom["stride"])
+            L2 = -(-(-(-L // S)) // S)
+            if P != F * NC + NC + L2 * NC * C + C:
+                raise ValueError("CNN bucket size does not match the geometry")
+            _lib.call("cfa_ge_grad_cnn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, C, F, NC, S, models.data_ptr(),
+                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), M, self.stream_handle(stream))
+        elif ml_model == 2:
+            H = int(geom["intermediate_nodes"])
+            if P != L * H + H + H * C + C:
+                raise ValueError("2NN bucket size does not match the geometry")
+            _lib.call("cfa_ge_grad_2nn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, H, C, models.data_ptr(),
+                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), M, self.stream_handle(stream))
+        else:
+            raise ValueError("ml_model must be 1 (CNN) or 2 (2NN)")
+        return grads
+
     # -- population ------------------------------------------------------------------------
     def mix_window(self, outs: Sequence[torch.Tensor], rows: Sequence[torch.Tensor], alphas: Sequence[Sequence[float]],
                    hl: int, hr: int, stream=None) -> None:
@@ -368,6 +403,26 @@ class Engine:
         _lib.call("cfa_mix_window_f32", _lib.ptr_table([o.data_ptr() for o in outs]),
                   _lib.ptr_table([r.data_ptr() for r in rows]), _lib.float_array(per_dev), nb, int(hl), int(hr), P,
                   self.stream_handle(stream))
+    def ge_population_step(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, state_ptrs: torch.Tensor,
+                           grad_ptrs: torch.Tensor, csr_ptr: torch.Tensor, csr_idx: torch.Tensor,
+                           csr_coef: torch.Tensor, D: int, rho: float, lr1: float, lr2: float, lr_split: int,
+                           use_filtered: bool, P: int, stream=None) -> None:
+        """cfa_ge_population_step_f32: stage-1 mix + MEWMA gradient step of D devices in one
+        launch; pointer tables are int64 CUDA tensors aligned with the CSR entries."""
+        for name, t, dt in (("out_ptrs", out_ptrs, torch.int64), ("src_ptrs", src_ptrs, torch.int64),
+                            ("state_ptrs", state_ptrs, torch.int64), ("grad_ptrs", grad_ptrs, torch.int64),
+                            ("csr_ptr", csr_ptr, torch.int32), ("csr_idx", csr_idx, torch.int32),
+                            ("csr_coef", csr_coef, torch.float32)):
+            if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+                raise TypeError(f"{name} must be a contiguous {dt} CUDA tensor")
+        E = csr_idx.numel()
+        if csr_ptr.numel() != D + 1 or out_ptrs.numel() != D or state_ptrs.numel() != E or grad_ptrs.numel() != E:
+            raise ValueError("tables: D+1 row pointers, D outputs, one state and one gradient slot per CSR entry")
+        _lib.call("cfa_ge_population_step_f32", out_ptrs.data_ptr(), src_ptrs.data_ptr(), state_ptrs.data_ptr(),
+                  grad_ptrs.data_ptr(), csr_ptr.data_ptr(), csr_idx.data_ptr(), csr_coef.data_ptr(), int(D),
+                  float(rho), float(lr1), float(lr2), int(lr_split), int(bool(use_filtered)), int(P),
+                  self.stream_handle(stream))
+
     def population(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
                    csr_idx: torch.Tensor, csr_coef: torch.Tensor, D: int, rule: int, P: int,
                    stream=None) -> None:

@@ -252,6 +252,17 @@ CFA_API int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L, in
                                 void* stream);
 CFA_API int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, int hidden, int classes,
                                 const float* models, float* grads, int M, void* stream);
+/* Population form: evaluation m uses model row model_row[m] of models [Dm, P] and data row
+ * data_row[m] of x [Dx, B, L] / y [Dx, B, classes] (DEVICE int32 tables), writing grads[m]. One
+ * launch evaluates every (device, neighbour) pair of a device-resident CFA-GE population: the
+ * gradient of device data_row[m]'s cost at device model_row[m]'s published model. */
+CFA_API int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,
+                                     int filter, int number, int stride, const float* models,
+                                     const int32_t* model_row, const int32_t* data_row, float* grads,
+                                     int M, void* stream);
+CFA_API int cfa_ge_grad_2nn_rows_f32(const float* x, const float* y, int B, int L, int hidden,
+                                     int classes, const float* models, const int32_t* model_row,
+                                     const int32_t* data_row, float* grads, int M, void* stream);
 
 /* (a1-a6 batched) Population round: one launch mixes D devices.
  * For device d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]) list its sources in order; the
@@ -263,6 +274,21 @@ CFA_API int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, in
 CFA_API int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,
                            const int32_t* csr_ptr, const int32_t* csr_idx,
                            const float* csr_coef, int D, int rule, size_t P, void* stream);
+
+/* (a4 batched) CFA-GE population step: stage 1 and the gradient step of every device of a
+ * device-resident population in one launch (cfa_ge_2stage.py:446-466, then :591-621). For device
+ * d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]): the first is its local model
+ * src_ptrs[csr_idx[e0]], the others its neighbours in order, mixed with the sequential rule and
+ * coefficient csr_coef[e]; then for each neighbour entry e, in order:
+ *   s <- rho * g + (1 - rho) * s   (s = state_ptrs[e], g = grad_ptrs[e], NULL = zero gradient)
+ *   w <- w - lr(i) * (use_filtered ? s : g),   lr(i) = i < lr_split ? lr1 : lr2
+ * and out_ptrs[d] = w. Every table is a DEVICE array; entry e0's state/grad slots are unused.
+ * Same operations, same order, same results as cfa_mix_population_f32 + cfa_mewma_update_f32. */
+CFA_API int cfa_ge_population_step_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                       float* const* state_ptrs, const float* const* grad_ptrs,
+                                       const int32_t* csr_ptr, const int32_t* csr_idx,
+                                       const float* csr_coef, int D, double rho, float lr1, float lr2,
+                                       size_t lr_split, int use_filtered, size_t P, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Multi-GPU (RCCL over xGMI): one process per GPU.

@@ -442,3 +442,57 @@ def tf1_2nn_grads(x, y, W1, b1, W2, b2):
     cost, dlog = _softmax_xent_grad(logits, y)
     dz = (dlog @ W2.T) * (act > 0)
     return [x.T @ dz, dz.sum(axis=0), act.T @ dlog, dlog.sum(axis=0)], cost
+
+
+def tf1_flat_shapes(ml_model: int, geom: dict):
+    """Per-tensor shapes of a TF1 model bucket (W1, b1, W2, b2) for the CFA-GE graphs."""
+    if ml_model == 1:
+        L2 = -(-(-(-geom["input_data"] // geom["stride"])) // geom["stride"])
+        return [(geom["filter"], 1, geom["number"]), (geom["number"],),
+                (L2 * geom["number"], geom["classes"]), (geom["classes"],)]
+    return [(geom["input_data"], geom["intermediate_nodes"]), (geom["intermediate_nodes"],),
+            (geom["intermediate_nodes"], geom["classes"]), (geom["classes"],)]
+
+
+def cfa_ge_population_round(W, pub_prev, G_prev, S, lists, x_all, y_all, ml_model, geom, eps, neighbors,
+                            rho, lr1, lr2):
+    """One 2-stage (fast) CFA-GE round, cfa_ge_2stage.py:388-621, for every device of a
+    population, on flat float64 buckets. Device i at epoch e:
+      stage 1 (:446-466): mix its local model W[i] with the neighbours' published models
+        pub_prev[j] (datamat{j}_{e-1}), alpha = eps * wf(i, j) with m = N-1;
+      (:468-471) publish its pre-mix model (the next round's pub[i] = W[i]);
+      (:491-535) gradients of its cost (x_all[i], y_all[i]) at each pub_prev[j] -> G_out[i, n];
+      (:564-621) for each neighbour n, j in order: slot i of datagrad{j}_{e-1}, i.e.
+        G_prev[j, m] with lists[j][m] == i (the last such m, as the slot assignment overwrites;
+        zeros if i is not j's neighbour), MEWMA into S[i, n] and the SGD step (filtered for the
+        CNN, raw for the 2NN).
+    Returns (W_new [D, P], S_new [D, N, P], G_out [D, N, P], pub_new [D, P])."""
+    W = np.asarray(W, np.float64)
+    D, P = W.shape
+    shapes = tf1_flat_shapes(ml_model, geom)
+    sizes = [int(np.prod(s)) for s in shapes]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    split = int(offs[2])
+    lr = np.where(np.arange(P) < split, lr1, lr2)
+    W_new = np.empty_like(W)
+    S_new = np.array(S, dtype=np.float64, copy=True)
+    G_out = np.zeros((D, max(len(l) for l in lists), P))
+    for i in range(D):
+        nb = [int(j) for j in lists[i]]
+        alphas = [eps * tf1_weight_factor(D, i, j, neighbors - 1) for j in nb]
+        w = tf1_mix_flat(np.asarray(W[i], np.float32).astype(np.float64), [np.asarray(pub_prev[j], np.float64) for j in nb],
+                         alphas)
+        for n, j in enumerate(nb):
+            m4 = [np.asarray(pub_prev[j], np.float64)[offs[k]:offs[k + 1]].reshape(shapes[k]) for k in range(4)]
+            if ml_model == 1:
+                g, _ = tf1_cnn_grads(x_all[i], y_all[i], *m4, stride=geom["stride"])
+            else:
+                g, _ = tf1_2nn_grads(x_all[i], y_all[i], *m4)
+            G_out[i, n] = np.concatenate([a.reshape(-1) for a in g])
+        for n, j in enumerate(nb):
+            slots = [m for m, k in enumerate(lists[j]) if int(k) == i]
+            g = np.asarray(G_prev[j, slots[-1]], np.float64) if slots else np.zeros(P)
+            S_new[i, n] = rho * g + (1 - rho) * S_new[i, n]
+            w = w - lr * (S_new[i, n] if ml_model == 1 else g)
+        W_new[i] = w
+    return W_new, S_new, G_out, W.copy()

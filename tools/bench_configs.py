@@ -134,8 +134,57 @@ def cpu_pool_round(P=25_000_000, K=8, workers=None, reps=3):
             "aggregate_GBps": round(workers * reps * (K + 2) * P * 4 / mix_time / 1e9, 2), "wall_s": round(wall, 1)}
 
 
+def cfa_ge_population(D=16, N=2, B=24, ml=1, rounds=50):
+    """Config 3 as a device-resident population (federated_amd.cfa_ge_population): one fast
+    CFA-GE round for all D devices = one stage-1 population launch, one gradient launch for all
+    D*N (device, neighbour) pairs, D MEWMA launches; against the oracle's float64 round on one
+    core (the repo's numpy path: per-device mix, gradients and MEWMA)."""
+    from federated_amd.cfa_ge_population import CfaGePopulation
+    eng = get_engine(0)
+    geom = ({"filter": 16, "number": 8, "stride": 5} if ml == 1 else {"intermediate_nodes": 32})
+    full = {**geom, "input_data": 512, "classes": 8}
+    rng = np.random.default_rng(3)
+    lists = T.kregular_tf1(D, N)
+    shapes = O.tf1_flat_shapes(ml, full)
+    P = sum(int(np.prod(s)) for s in shapes)
+    x = rng.standard_normal((D, B, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[rng.integers(0, 8, (D, B))]
+    pop = CfaGePopulation(eng, ml, geom, torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda(), lists, 1.0, N,
+                          0.99, 0.1, 0.1)
+    W = (rng.standard_normal((D, P)) * 0.1).astype(np.float32)
+    pop.load(torch.from_numpy(W).cuda(), torch.from_numpy(W).cuda())
+    for _ in range(5):
+        pop.round()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(rounds):
+        pop.round()
+    e1.record()
+    torch.cuda.synchronize()
+    host_us = (time.perf_counter() - t0) / rounds * 1e6
+    gpu_us = e0.elapsed_time(e1) / rounds * 1e3
+    Nm = max(len(l) for l in lists)
+    Wd = W.astype(np.float64)
+    G = np.zeros((D, Nm, P))
+    S = np.zeros((D, Nm, P))
+    t = med_time(lambda: O.cfa_ge_population_round(Wd, Wd, G, S, lists, x, y, ml, full, 1.0, N, 0.99, 0.1, 0.1), 3)
+    return {"devices": D, "neighbours": N, "samples": B, "P": P, "model": "cnn" if ml == 1 else "2nn",
+            "round_us_gpu_events": round(gpu_us, 1), "round_us_host": round(host_us, 1),
+            "numpy_round_ms_1core": round(t * 1e3, 2), "speedup_vs_numpy": round(t * 1e6 / host_us, 1)}
+
+
 def main():
     rows = []
+    if len(sys.argv) > 1 and sys.argv[1] == "c3":
+        rows.append({"config": "C3 CFA-GE CNN, 16 devices, N=2, device-resident population round",
+                     **cfa_ge_population()})
+        rows.append({"config": "C3 shapes with the 2NN model, 16 devices, N=2, device-resident population round",
+                     **cfa_ge_population(ml=2)})
+        for r in rows:
+            print(json.dumps(r), flush=True)
+        return
     rows.append({"config": "CPU pool baseline: 8 x 25M mix, one process per device", **cpu_pool_round()})
     rows.append({"config": "C1 2NN, 4 devices, cfa.py (federated_sample_2NN_CFA.py)",
                  **tf1_call([(512, 32), (32,), (32, 8), (8,)], 4, 2, "cfa")})
