@@ -81,10 +81,13 @@ SIGNATURES = {
                                      _c_void_p, _c_void_p, _c_int, _c_void_p]),
     "cfa_ge_grad_2nn_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p, _c_void_p,
                                      _c_int, _c_void_p]),
+    "cfa_ge_grad_workspace_elems": (_c_size_t, [_c_int, _c_int, _c_size_t]),
     "cfa_ge_grad_cnn_rows_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p]),
+                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_size_t,
+                                          _c_int, _c_void_p]),
     "cfa_ge_grad_2nn_rows_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p,
-                                          _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p]),
+                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int,
+                                          _c_void_p]),
     "cfa_ge_population_step_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                             _c_void_p, _c_int, ctypes.c_double, ctypes.c_float, ctypes.c_float,
                                             _c_size_t, _c_int, _c_size_t, _c_void_p]),

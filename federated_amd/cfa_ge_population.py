@@ -88,6 +88,7 @@ class CfaGePopulation:
         # gradient evaluations: pair (i, n) -> model row lists[i][n] of pub, data row i
         mrow = [j for i, nb in enumerate(self.lists) for j in nb + [0] * (Nmax - len(nb))]
         drow = [i for i, nb in enumerate(self.lists) for _ in range(Nmax)]
+        self._ws = engine.grad_workspace(len(mrow), int(x.shape[1]), P)  # batch split over workgroups
         self._mrow = torch.tensor(mrow, dtype=torch.int32, device=dev)
         self._drow = torch.tensor(drow, dtype=torch.int32, device=dev)
         # where device i finds slot i of neighbour j's gradients: G row j*N + m (last m with
@@ -150,7 +151,7 @@ class CfaGePopulation:
         src, dst = self._tables[self._rot]
         # 4: gradients of every device's cost at its neighbours' previous-round models
         eng.grad_rows(self.ml_model, self.x, self.y, self.pub, self._mrow, self._drow, self.G_next,
-                      self.geom, stream)
+                      self.geom, stream, workspace=self._ws)
         # 1 + 3: stage-1 mix and the gradient step with the previous round's gradients, one launch
         eng.ge_population_step(dst, src, self._states, self._grads[self._gpar], ptr, idx, coef, D, self.rho,
                                self.lr1, self.lr2, self.lr_split, self.ml_model == 1, P, stream)

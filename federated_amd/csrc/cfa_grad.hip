@@ -89,6 +89,7 @@ struct CnnDims {
   int B, L, C, F, NC, S;
   int L1, L2, pl, ql;  // conv / pool output lengths, left pads
   int Bc;              // samples per LDS-resident chunk
+  int Bs;              // samples per workgroup (grid.y splits the batch; partial sums go to a workspace)
   long long P;         // parameters per model
 };
 
@@ -136,7 +137,10 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   const long long dr = drow ? drow[blockIdx.x] : 0;
   x += dr * d.B * d.L;
   y += dr * d.B * d.C;
-  float* g = grads + (long long)blockIdx.x * d.P;
+  // grid.y splits the batch: this workgroup sums samples [bb, be) into its own partial bucket
+  // (gridDim.y == 1: the model's gradient bucket itself)
+  float* g = grads + ((long long)blockIdx.x * gridDim.y + blockIdx.y) * d.P;
+  const int bb = blockIdx.y * d.Bs, be = min(d.B, bb + d.Bs);
   const int tid = threadIdx.x, T = blockDim.x;
   float* gW2 = g + nG1;
   float* gb2 = gW2 + nW2;
@@ -152,9 +156,13 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   float wreg[kMaxTaps];
 #pragma unroll
   for (int k = 0; k < kMaxTaps; ++k) wreg[k] = (taps_in_regs && k < d.F) ? W1[k * d.NC + tid % d.NC] : 0.f;
-  for (int b0 = 0; b0 < d.B; b0 += d.Bc) {
-    const int nb = min(d.Bc, d.B - b0);
-    const bool first = b0 == 0;
+  if (bb >= be) {  // no sample left for this split: a zero partial
+    for (long long i = threadIdx.x; i < d.P; i += blockDim.x) g[i] = 0.f;
+    return;
+  }
+  for (int b0 = bb; b0 < be; b0 += d.Bc) {
+    const int nb = min(d.Bc, be - b0);
+    const bool first = b0 == bb;
     stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
     stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
     __syncthreads();
@@ -295,6 +303,7 @@ struct NnDims {
   int B, L, H, C;
   int G;   // ceil(L / kSpan) slices of the input dimension for the first layer's partial sums
   int Bc;
+  int Bs;  // samples per workgroup (grid.y splits the batch; partial sums go to a workspace)
   long long P;
 };
 
@@ -323,7 +332,10 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
   x += dr * d.B * d.L;
   y += dr * d.B * d.C;
   const float* W1 = m;             // [L][H], read from global once per launch (kept in registers)
-  float* g = grads + (long long)blockIdx.x * d.P;
+  // grid.y splits the batch: this workgroup sums samples [bb, be) into its own partial bucket
+  // (gridDim.y == 1: the model's gradient bucket itself)
+  float* g = grads + ((long long)blockIdx.x * gridDim.y + blockIdx.y) * d.P;
+  const int bb = blockIdx.y * d.Bs, be = min(d.B, bb + d.Bs);
   float* gW1 = g;
   float* gb1 = gW1 + nW1;
   float* gW2 = gb1 + d.H;
@@ -344,9 +356,13 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
     for (int u = 0; u < kSpan; ++u)
       wreg[u] = (w_in_regs && grp < d.G && i0 + u < d.L) ? W1[(long long)(i0 + u) * d.H + h] : 0.f;
   }
-  for (int b0 = 0; b0 < d.B; b0 += d.Bc) {
-    const int nb = min(d.Bc, d.B - b0);
-    const bool first = b0 == 0;
+  if (bb >= be) {  // no sample left for this split: a zero partial
+    for (long long i = threadIdx.x; i < d.P; i += blockDim.x) g[i] = 0.f;
+    return;
+  }
+  for (int b0 = bb; b0 < be; b0 += d.Bc) {
+    const int nb = min(d.Bc, be - b0);
+    const bool first = b0 == bb;
     stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
     stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
     __syncthreads();
@@ -495,9 +511,36 @@ int plan_chunk(const void* kernel, long long fixed, long long per_sample, int B,
 
 namespace {
 
+// Sum of the Sp partial buckets of each evaluation, in split order (deterministic).
+__global__ __launch_bounds__(kBlock) void reduce_splits_kernel(const float* __restrict__ ws,
+                                                               float* __restrict__ grads, int Sp,
+                                                               long long P) {
+  const long long m = blockIdx.y;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += (long long)gridDim.x * kBlock) {
+    float s = ws[(m * Sp) * P + i];
+    for (int sp = 1; sp < Sp; ++sp) s += ws[(m * Sp + sp) * P + i];
+    grads[m * P + i] = s;
+  }
+}
+
+// Batch split for M evaluations of B samples of P-parameter models: about two workgroups per CU
+// in all, at most 8 per evaluation, and fewer for larger models, whose partial buckets (written
+// and re-read by the reduction) and per-workgroup weight staging grow with P. Measured at the
+// CFA-GE shapes (tools/probe/grad_split_sweep.sh, 32 evaluations of 24 samples): CNN (P = 1 488)
+// 41.5 -> 17.0 us at 8 splits, 2NN (P = 16 680) 28.5 -> 21.3 us at 3, both slower past that.
+int batch_split(int M, int B, long long P) {
+  if (M <= 0 || B <= 1) return 1;
+  int want = (2 * device_cus() + M - 1) / M;
+  want = std::min<long long>(want, std::min<long long>(8, std::max<long long>(1, 65536 / std::max<long long>(P, 1))));
+  if (const char* e = getenv("CFA_GRAD_SPLIT")) want = std::max(1, atoi(e));  // measurement knob
+  int sp = std::max(1, std::min(B, want));
+  const int bs = (B + sp - 1) / sp;
+  return (B + bs - 1) / bs;
+}
+
 int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L, int classes, int filter,
                     int number, int stride, const float* models, const int* mrow, const int* drow,
-                    float* grads, int M, void* stream) {
+                    float* grads, float* ws, size_t ws_elems, int M, void* stream) {
   if (M < 0 || B < 1 || L < 1 || classes < 1 || filter < 1 || number < 1 || stride < 1)
     return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d C %d F %d NC %d S %d M %d)", fn, B, L, classes,
                 filter, number, stride, M);
@@ -518,15 +561,27 @@ int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L
   d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), B, &bytes);
   if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  int Sp = batch_split(M, B, d.P);
+  if (!ws || ws_elems < (size_t)M * Sp * (size_t)d.P) Sp = 1;
+  d.Bs = (B + Sp - 1) / Sp;
+  float* out = Sp > 1 ? ws : grads;
+  const dim3 grid((unsigned)M, (unsigned)Sp);
   if (fast)
-    grad_cnn_kernel<16, 5><<<M, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, grads, d);
+    grad_cnn_kernel<16, 5><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out, d);
   else
-    grad_cnn_kernel<0, 0><<<M, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, grads, d);
-  return check_launch("grad_cnn_kernel");
+    grad_cnn_kernel<0, 0><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out, d);
+  if (int rc = check_launch("grad_cnn_kernel")) return rc;
+  if (Sp > 1) {
+    reduce_splits_kernel<<<dim3((unsigned)std::min<long long>((d.P + kBlock - 1) / kBlock, 64), (unsigned)M), kBlock,
+                           0, st>>>(ws, grads, Sp, d.P);
+    return check_launch("reduce_splits_kernel");
+  }
+  return CFA_OK;
 }
 
 int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L, int hidden, int classes,
-                    const float* models, const int* mrow, const int* drow, float* grads, int M, void* stream) {
+                    const float* models, const int* mrow, const int* drow, float* grads, float* ws,
+                    size_t ws_elems, int M, void* stream) {
   if (M < 0 || B < 1 || L < 1 || hidden < 1 || classes < 1)
     return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d H %d C %d M %d)", fn, B, L, hidden, classes, M);
   if (M == 0) return CFA_OK;
@@ -538,9 +593,20 @@ int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L
   long long bytes = 0;
   d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), B, &bytes);
   if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
-  grad_2nn_kernel<<<M, kGradBlock, (size_t)bytes, static_cast<hipStream_t>(stream)>>>(x, y, models, mrow, drow,
-                                                                                     grads, d);
-  return check_launch("grad_2nn_kernel");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int Sp = batch_split(M, B, d.P);
+  if (!ws || ws_elems < (size_t)M * Sp * (size_t)d.P) Sp = 1;
+  d.Bs = (B + Sp - 1) / Sp;
+  float* out = Sp > 1 ? ws : grads;
+  grad_2nn_kernel<<<dim3((unsigned)M, (unsigned)Sp), kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out,
+                                                                                       d);
+  if (int rc = check_launch("grad_2nn_kernel")) return rc;
+  if (Sp > 1) {
+    reduce_splits_kernel<<<dim3((unsigned)std::min<long long>((d.P + kBlock - 1) / kBlock, 64), (unsigned)M), kBlock,
+                           0, st>>>(ws, grads, Sp, d.P);
+    return check_launch("reduce_splits_kernel");
+  }
+  return CFA_OK;
 }
 
 }  // namespace
@@ -549,31 +615,38 @@ extern "C" int cfa_ge_grad_cnn_f32(const float* x, const float* y, int B, int L,
                                    int filter, int number, int stride, const float* models,
                                    float* grads, int M, void* stream) {
   return launch_grad_cnn("cfa_ge_grad_cnn_f32", x, y, B, L, classes, filter, number, stride, models, nullptr,
-                         nullptr, grads, M, stream);
+                         nullptr, grads, nullptr, 0, M, stream);
 }
 
 extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, int hidden,
                                    int classes, const float* models, float* grads, int M,
                                    void* stream) {
-  return launch_grad_2nn("cfa_ge_grad_2nn_f32", x, y, B, L, hidden, classes, models, nullptr, nullptr, grads, M,
-                         stream);
+  return launch_grad_2nn("cfa_ge_grad_2nn_f32", x, y, B, L, hidden, classes, models, nullptr, nullptr, grads,
+                         nullptr, 0, M, stream);
+}
+
+extern "C" size_t cfa_ge_grad_workspace_elems(int M, int B, size_t P) {
+  const int sp = batch_split(M, B, (long long)P);
+  return sp > 1 ? (size_t)M * sp * P : 0;
 }
 
 extern "C" int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,
                                         int filter, int number, int stride, const float* models,
                                         const int32_t* model_row, const int32_t* data_row,
-                                        float* grads, int M, void* stream) {
+                                        float* grads, float* workspace, size_t workspace_elems, int M,
+                                        void* stream) {
   if (M > 0 && (!model_row || !data_row))
     return fail(CFA_E_INVALID, "cfa_ge_grad_cnn_rows_f32: null row table");
   return launch_grad_cnn("cfa_ge_grad_cnn_rows_f32", x, y, B, L, classes, filter, number, stride, models,
-                         model_row, data_row, grads, M, stream);
+                         model_row, data_row, grads, workspace, workspace_elems, M, stream);
 }
 
 extern "C" int cfa_ge_grad_2nn_rows_f32(const float* x, const float* y, int B, int L, int hidden,
                                         int classes, const float* models, const int32_t* model_row,
-                                        const int32_t* data_row, float* grads, int M, void* stream) {
+                                        const int32_t* data_row, float* grads, float* workspace,
+                                        size_t workspace_elems, int M, void* stream) {
   if (M > 0 && (!model_row || !data_row))
     return fail(CFA_E_INVALID, "cfa_ge_grad_2nn_rows_f32: null row table");
   return launch_grad_2nn("cfa_ge_grad_2nn_rows_f32", x, y, B, L, hidden, classes, models, model_row, data_row,
-                         grads, M, stream);
+                         grads, workspace, workspace_elems, M, stream);
 }

@@ -345,12 +345,18 @@ class Engine:
                   grads.data_ptr(), M, self.stream_handle(stream))
         return grads
 
+    def grad_workspace(self, M: int, B: int, P: int) -> torch.Tensor:
+        """Workspace for the batch-split gradient launch (cfa_ge_grad_workspace_elems)."""
+        n = int(_lib.load().cfa_ge_grad_workspace_elems(int(M), int(B), int(P)))
+        return torch.empty(max(n, 1), dtype=torch.float32, device=self.device)
+
     def grad_rows(self, ml_model: int, x: torch.Tensor, y: torch.Tensor, models: torch.Tensor,
                   model_row: torch.Tensor, data_row: torch.Tensor, grads: torch.Tensor, geom: dict,
-                  stream=None) -> torch.Tensor:
+                  stream=None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Population form (cfa_ge_grad_{cnn,2nn}_rows_f32): evaluation m = gradient of data row
         data_row[m] (x [Dx, B, L], y [Dx, B, C]) at model row model_row[m] of models [Dm, P],
-        into grads [M, P]. ``geom``: filter/number/stride (CNN) or intermediate_nodes (2NN)."""
+        into grads [M, P]. ``geom``: filter/number/stride (CNN) or intermediate_nodes (2NN).
+        ``workspace`` (``grad_workspace``) lets each evaluation's batch spread over workgroups."""
         for name, t, nd in (("x", x, 3), ("y", y, 3)):
             if not t.is_cuda or t.dtype != torch.float32 or t.dim() != nd or not t.is_contiguous():
                 raise TypeError(f"{name} must be a contiguous 3-D fp32 CUDA tensor")
@@ -363,19 +369,26 @@ class Engine:
         if tuple(y.shape[:2]) != (Dx, B) or Pg != P:
             raise ValueError("y must be [Dx, B, C] and grads [M, P]")
         C = int(y.shape[2])
+        ws_ptr, ws_n = None, 0
+        if workspace is not None:
+            if not workspace.is_cuda or workspace.dtype != torch.float32 or not workspace.is_contiguous():
+                raise TypeError("workspace must be a contiguous fp32 CUDA tensor")
+            ws_ptr, ws_n = workspace.data_ptr(), workspace.numel()
         if ml_model == 1:
             F, NC, S = int(geom["filter"]), int(geom["number"]), int(geom["stride"])
             L2 = -(-(-(-L // S)) // S)
             if P != F * NC + NC + L2 * NC * C + C:
                 raise ValueError("CNN bucket size does not match the geometry")
             _lib.call("cfa_ge_grad_cnn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, C, F, NC, S, models.data_ptr(),
-                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), M, self.stream_handle(stream))
+                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), ws_ptr, ws_n, M,
+                      self.stream_handle(stream))
         elif ml_model == 2:
             H = int(geom["intermediate_nodes"])
             if P != L * H + H + H * C + C:
                 raise ValueError("2NN bucket size does not match the geometry")
             _lib.call("cfa_ge_grad_2nn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, H, C, models.data_ptr(),
-                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), M, self.stream_handle(stream))
+                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), ws_ptr, ws_n, M,
+                      self.stream_handle(stream))
         else:
             raise ValueError("ml_model must be 1 (CNN) or 2 (2NN)")
         return grads

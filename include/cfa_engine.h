@@ -255,14 +255,19 @@ CFA_API int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, in
 /* Population form: evaluation m uses model row model_row[m] of models [Dm, P] and data row
  * data_row[m] of x [Dx, B, L] / y [Dx, B, classes] (DEVICE int32 tables), writing grads[m]. One
  * launch evaluates every (device, neighbour) pair of a device-resident CFA-GE population: the
- * gradient of device data_row[m]'s cost at device model_row[m]'s published model. */
+ * gradient of device data_row[m]'s cost at device model_row[m]'s published model. With a device
+ * `workspace` of at least cfa_ge_grad_workspace_elems(M, B, P) floats, each evaluation's batch is
+ * split over several workgroups (about two per CU in all) whose partial sums are then added in a
+ * fixed order (deterministic); with less (or NULL) one workgroup takes each evaluation. */
+CFA_API size_t cfa_ge_grad_workspace_elems(int M, int B, size_t P);
 CFA_API int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,
                                      int filter, int number, int stride, const float* models,
                                      const int32_t* model_row, const int32_t* data_row, float* grads,
-                                     int M, void* stream);
+                                     float* workspace, size_t workspace_elems, int M, void* stream);
 CFA_API int cfa_ge_grad_2nn_rows_f32(const float* x, const float* y, int B, int L, int hidden,
                                      int classes, const float* models, const int32_t* model_row,
-                                     const int32_t* data_row, float* grads, int M, void* stream);
+                                     const int32_t* data_row, float* grads, float* workspace,
+                                     size_t workspace_elems, int M, void* stream);
 
 /* (a1-a6 batched) Population round: one launch mixes D devices.
  * For device d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]) list its sources in order; the

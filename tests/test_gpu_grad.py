@@ -81,3 +81,40 @@ def test_bad_geometry_is_refused(gpu):
     y = np.eye(8, dtype=np.float32)[[0, 1]]
     with pytest.raises(ValueError):
         T.gradients_batched(1, x, y, models, stride=5)
+
+
+@pytest.mark.parametrize("ml,B,M", [(1, 24, 3), (2, 24, 3), (1, 5, 40), (2, 100, 2)])
+def test_rows_form_with_and_without_batch_split(gpu, ml, B, M):
+    """cfa_ge_grad_*_rows_f32: evaluation m = data row drow[m] at model row mrow[m]; with a
+    workspace the batch is split over workgroups and summed in a second pass."""
+    import torch
+    rng = np.random.default_rng(ml * 100 + B + M)
+    Dx, Dm = 3, 4
+    if ml == 1:
+        geom = {"filter": 16, "number": 8, "stride": 5}
+        models = _cnn_models(rng, Dm)
+        ref_fn = lambda xi, yi, m: orc.tf1_cnn_grads(xi, yi, *m, stride=5)
+    else:
+        geom = {"intermediate_nodes": 32}
+        models = [[(rng.standard_normal((512, 32)) * 0.1).astype(np.float32), (rng.standard_normal(32) * 0.1).astype(np.float32),
+                   (rng.standard_normal((32, 8)) * 0.3).astype(np.float32), (rng.standard_normal(8) * 0.1).astype(np.float32)]
+                  for _ in range(Dm)]
+        ref_fn = lambda xi, yi, m: orc.tf1_2nn_grads(xi, yi, *m)
+    flat = np.stack([np.concatenate([a.reshape(-1) for a in m]) for m in models])
+    P = flat.shape[1]
+    x = rng.standard_normal((Dx, B, 512)).astype(np.float32)
+    y = np.eye(8, dtype=np.float32)[rng.integers(0, 8, (Dx, B))]
+    mrow = rng.integers(0, Dm, M).astype(np.int32)
+    drow = rng.integers(0, Dx, M).astype(np.int32)
+    t = lambda a: torch.from_numpy(a).cuda()
+    outs = []
+    for ws in (None, gpu.grad_workspace(M, B, P)):
+        g = torch.empty(M, P, device="cuda")
+        gpu.grad_rows(ml, t(x), t(y), t(flat), t(mrow), t(drow), g, geom, workspace=ws)
+        outs.append(g.cpu().numpy())
+    offs = np.concatenate([[0], np.cumsum([a.size for a in models[0]])])
+    for out in outs:
+        for m in range(M):
+            ref, _ = ref_fn(x[drow[m]], y[drow[m]], models[mrow[m]])
+            for k in range(4):
+                assert normwise_close(out[m, offs[k]:offs[k + 1]], ref[k].reshape(-1), 1e-5), (m, k)
