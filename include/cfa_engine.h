@@ -9,7 +9,10 @@
  *
  * Conventions
  *   - Plain pointers and sizes only. Buffers are caller-owned device pointers
- *     (hipMalloc / PyTorch-ROCm tensors). The library allocates nothing on the hot path.
+ *     (hipMalloc / PyTorch-ROCm tensors). The library allocates no device memory on the hot
+ *     path (scratch comes from the caller, e.g. the gradient workspace; the one exception is
+ *     cfa_mix_tf1_f32 above CFA_MAX_FANIN neighbours, documented there). The host-only MQTT
+ *     payload codec allocates its parse tree in host memory (freed by cfa_payload_free).
  *   - `stream` is a hipStream_t passed as void*; NULL means the legacy default stream.
  *     Every compute call is asynchronous on that stream.
  *   - Return 0 on success, a negative CFA_E* code on failure. `cfa_last_error()` returns a
