@@ -436,3 +436,58 @@ def test_mix_seq_bucket_larger_than_2gib(gpu):
         assert np.array_equal(out[sl].cpu().numpy(), ref), a
     del local, nb, out
     torch.cuda.empty_cache()
+
+
+def _special(rng, P, dtype=np.float32):
+    """Random values salted with the IEEE specials numpy meets in real weights: NaN, +-inf,
+    -0.0, subnormals, the largest finite values."""
+    fi = np.finfo(dtype)
+    a = rng.standard_normal(P).astype(dtype)
+    specials = np.array([np.nan, np.inf, -np.inf, -0.0, 0.0, fi.smallest_subnormal, -fi.smallest_subnormal,
+                         fi.smallest_normal * 0.5, fi.tiny, fi.max, -fi.max, 1e-40 if dtype == np.float32 else 1e-310],
+                        dtype=dtype)
+    idx = rng.choice(P, size=min(P, 3 * len(specials)), replace=False)
+    a[idx] = np.resize(specials, idx.size)
+    return a
+
+
+def _same_bits_or_nan(got, ref):
+    """Bitwise equal, except that any NaN matches any NaN (payloads are not specified)."""
+    got, ref = np.asarray(got), np.asarray(ref)
+    both_nan = np.isnan(got) & np.isnan(ref)
+    gi = got.view(np.uint32 if got.dtype == np.float32 else np.uint64)
+    ri = ref.view(np.uint32 if ref.dtype == np.float32 else np.uint64)
+    return bool(np.all(both_nan | (gi == ri)))
+
+
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_special_values_follow_numpy(gpu, n):
+    """NaN / inf / -0.0 / subnormal inputs: the fp32 sequential rule, the FedAvg divisor rule and
+    the TF1 fp64 chain give numpy's results (no flush-to-zero, IEEE inf/NaN propagation)."""
+    rng = np.random.default_rng(700 + n)
+    P = 4096 + 5
+    local = _special(rng, P)
+    nbrs = [_special(rng, P) for _ in range(n)]
+    alphas = [1.0 / (n + 1)] * n
+    with np.errstate(all="ignore"):
+        ref = O.sequential_mix(local, nbrs, alphas)
+    out = torch.empty(P, dtype=torch.float32, device="cuda")
+    gpu.mix_seq(out, _dev(local), [_dev(x) for x in nbrs], alphas)
+    assert _same_bits_or_nan(out.cpu().numpy(), ref)
+    # FedAvg form p + u * (x - p) / C
+    with np.errstate(all="ignore"):
+        w = local.copy()
+        for x in nbrs:
+            w = w + np.float32(1.0) * (x - w) / np.float32(n)
+    out2 = torch.empty(P, dtype=torch.float32, device="cuda")
+    gpu.mix_seq_div(out2, _dev(local), [_dev(x) for x in nbrs], [1.0] * n, [float(n)] * n)
+    assert _same_bits_or_nan(out2.cpu().numpy(), w)
+    # TF1 fp64 chain on fp64 buckets of fp64 specials
+    l64 = _special(rng, P, np.float64)
+    n64 = [_special(rng, P, np.float64) for _ in range(n)]
+    a64 = [0.5 / (k + 1) for k in range(n)]
+    with np.errstate(all="ignore"):
+        r64 = O.tf1_mix_flat(l64, n64, a64)
+    o64 = torch.empty(P, dtype=torch.float64, device="cuda")
+    gpu.mix_tf1_f64(o64, _dev(l64), [_dev(x) for x in n64], a64, False)
+    assert _same_bits_or_nan(o64.cpu().numpy(), r64)
