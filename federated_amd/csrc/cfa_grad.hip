@@ -484,12 +484,45 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
 
 // Dynamic LDS for one workgroup: up to 64 KiB by default; above that the kernel's limit is
 // raised to the device's (160 KiB on gfx950) when the runtime allows it.
-int device_lds_max() {
+int device_lds_max() {  // per device, cached after the first query
+  static int cache[64] = {0};
   int dev = 0, v = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 65536;
-  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0)
-    return 65536;
+  if (dev >= 0 && dev < 64) {
+    const int c = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+    if (c > 0) return c;
+  }
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0) v = 65536;
+  if (dev >= 0 && dev < 64) __atomic_store_n(&cache[dev], v, __ATOMIC_RELAXED);
   return v;
+}
+
+// Raise a kernel's dynamic-LDS limit to `bytes` once per (kernel, device); false if refused.
+bool raise_lds_limit(const void* kernel, int bytes) {
+  static const void* keys[8] = {nullptr};
+  static int granted[8][64] = {{0}};  // per kernel slot and device: the limit granted so far
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = -1;
+  int slot = -1;
+  for (int i = 0; i < 8 && dev >= 0; ++i) {
+    const void* k = __atomic_load_n(&keys[i], __ATOMIC_ACQUIRE);
+    if (k == kernel) { slot = i; break; }
+    if (!k) {
+      const void* expected = nullptr;
+      if (__atomic_compare_exchange_n(&keys[i], &expected, kernel, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE) ||
+          expected == kernel) {
+        slot = i;
+        break;
+      }
+    }
+  }
+  if (slot >= 0 && __atomic_load_n(&granted[slot][dev], __ATOMIC_RELAXED) >= bytes) return true;
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (slot >= 0) __atomic_store_n(&granted[slot][dev], bytes, __ATOMIC_RELAXED);
+  return true;
 }
 
 // Samples per chunk for `fixed` + Bc * `per_sample` floats of LDS; sets *bytes. 0 if not even one fits.
@@ -498,11 +531,7 @@ int plan_chunk(const void* kernel, long long fixed, long long per_sample, int B,
   if (const char* cap = getenv("CFA_GRAD_LDS_CAP")) limit = std::min<long long>(limit, atoll(cap));  // measurement knob
   auto fit = [&](long long lim) { return (int)std::min<long long>(B, (lim / 4 - fixed) / per_sample); };
   int bc = fit(limit);
-  if (4 * (fixed + per_sample * bc) > 65536 &&
-      hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)limit) != hipSuccess) {
-    (void)hipGetLastError();
-    bc = fit(65536);
-  }
+  if (4 * (fixed + per_sample * bc) > 65536 && !raise_lds_limit(kernel, (int)limit)) bc = fit(65536);
   *bytes = 4 * (fixed + per_sample * std::max(bc, 0));
   return std::max(bc, 0);
 }
