@@ -1,5 +1,7 @@
 // cfa_mewma.hip — CFA-GE gradient-bucket update on fp32 buckets (MEWMA filter + SGD step with the
 // neighbours' gradients), TF1/consensus/cfa_ge_2stage.py:329-371 and :593-621.
+#include <utility>
+
 #include "cfa_internal.h"
 
 namespace {
@@ -18,29 +20,42 @@ struct MewmaArgs {
   int init, filtered;
 };
 
-// Contiguous case: float4 per lane, g and s streamed once each.
+// Contiguous case: float4 per lane, g and s streamed once each. The fan-in N is a template
+// parameter, so every g and s load of a vector is issued before the first update uses it.
+template <int N>
 __global__ __launch_bounds__(kBlock) void mewma_vec_kernel(MewmaArgs a, long long nvec) {
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
        i += (long long)gridDim.x * kBlock) {
-    f4 W = ld4<false>(a.W, i);
+    f4 W = ld4<true>(a.W, i);
+    f4 g[N], s_old[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      g[j] = ld4<true>(a.g[j], i);
+      if (!a.init) s_old[j] = ld4<true>(a.s[j], i);
+    }
     const long long e0 = i * 4;
     f4 lr;
 #pragma unroll
     for (int c = 0; c < 4; ++c) lr[c] = (e0 + c) < a.split ? a.lr1 : a.lr2;
-    for (int j = 0; j < a.n; ++j) {
-      const f4 g = ld4<false>(a.g[j], i);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
       f4 s;
       if (a.init) {
-        s = g;
+        s = g[j];
       } else {
-        const f4 s_old = ld4<false>(a.s[j], i);
-        s = a.rho * g + a.one_minus_rho * s_old;  // numpy: rho*g + (1-rho)*s
+        s = a.rho * g[j] + a.one_minus_rho * s_old[j];  // numpy: rho*g + (1-rho)*s
       }
-      st4<false>(a.s[j], i, s);
-      W = W - lr * (a.filtered ? s : g);
+      st4<true>(a.s[j], i, s);
+      W = W - lr * (a.filtered ? s : g[j]);
     }
-    st4<false>(a.W, i, W);
+    st4<true>(a.W, i, W);
   }
+}
+
+template <int... Ns>
+static void launch_mewma_vec(int m, unsigned grid, hipStream_t st, const MewmaArgs& a, long long nvec,
+                             std::integer_sequence<int, Ns...>) {
+  ((m == Ns + 1 ? (void)(mewma_vec_kernel<Ns + 1><<<grid, kBlock, 0, st>>>(a, nvec)) : (void)0), ...);
 }
 
 // Generic case: scalar, arbitrary element stride on the gradient buckets.
@@ -103,7 +118,8 @@ extern "C" int cfa_mewma_update_f32(float* W, float* const* s, const float* cons
     if (vec) {
       const long long nvec = (long long)P / 4;
       if (nvec > 0) {
-        mewma_vec_kernel<<<grid_for((nvec + kBlock - 1) / kBlock), kBlock, 0, st>>>(a, nvec);
+        launch_mewma_vec(m, grid_for((nvec + kBlock - 1) / kBlock), st, a, nvec,
+                         std::make_integer_sequence<int, CFA_MAX_FANIN>{});
         if (int rc = check_launch("mewma_vec")) return rc;
       }
       begin = nvec * 4;

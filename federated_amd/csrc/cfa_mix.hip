@@ -121,12 +121,20 @@ __global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFa
   if (compress) block_add_count(kept, cp.kept);
 }
 
-// Standalone compression epilogue (no mixing): y in place.
+// Standalone compression epilogue (no mixing): y in place. Vectors [0, nvec) move 16 bytes per
+// lane (y and ref 16-byte aligned), elements [4 * nvec, P) one at a time.
 __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float* ref, long long P,
-                                                          CompressParams cp) {
+                                                          long long nvec, CompressParams cp) {
   unsigned kept = 0;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
-       i += (long long)gridDim.x * kBlock) {
+  const long long stride = (long long)gridDim.x * kBlock;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride) {
+    f4 v = ld4<true>(y, i);
+    const f4 r = ref ? ld4<true>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = compress_one(v[c], r[c], cp, kept);
+    st4<true>(y, i, v);
+  }
+  for (long long i = 4 * nvec + (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += stride) {
     const float r = ref ? ref[i] : 0.0f;
     y[i] = compress_one(y[i], r, cp, kept);
   }
@@ -442,8 +450,10 @@ extern "C" int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, s
   cp.cend = (long long)P;
   cp.kept = kept_count;
   hipStream_t st = (hipStream_t)stream;
-  compress_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
-      y, ref, (long long)P, cp);
+  const bool vec = (addr(y) & 15) == 0 && (!ref || (addr(ref) & 15) == 0);
+  const long long nvec = vec ? (long long)P / 4 : 0;
+  compress_kernel<<<grid_for(((vec ? nvec : (long long)P) + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+      y, ref, (long long)P, nvec, cp);
   return check_launch("compress");
 }
 

@@ -4,6 +4,8 @@
 // 225-273, cfa_ge_2stage.py:76-83, 331-371, 593-621; the fp64 server-side folds of
 // FL_over_MQTT/PS_server.py:130-133, learner_consensus.py:151-152,
 // federated_sample_CNN_CFA_FA.py:86-89, 130-133, 280-283.
+#include <utility>
+
 #include "cfa_internal.h"
 
 namespace {
@@ -131,6 +133,79 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fan
   if (compress) block_add_count(kept, cp.kept);
 }
 
+// Vector form of mix_tf1_f64_kernel for 16-byte-aligned buckets: each lane moves two doubles per
+// bucket per vector, U vectors per tile, every load of a tile issued before its first use, the
+// fan-in N and the rule at compile time (the runtime loop above serialises its loads).
+typedef double d2 __attribute__((ext_vector_type(2)));
+template <int N, int RULE, bool STEP0F32>
+__global__ __launch_bounds__(kBlock) void fold_f64_vec_kernel(double* out, F64Fanin f, long long nvec2,
+                                                               const double* ref, CompressParams cp,
+                                                               int compress) {
+  constexpr int U = 2;
+  constexpr long long kTile = (long long)kBlock * U;
+  unsigned kept = 0;
+  for (long long t = blockIdx.x; t * kTile < nvec2; t += gridDim.x) {
+    long long idx[U];
+    bool ok[U];
+    d2 v[U][N + 1];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      idx[u] = t * kTile + (long long)u * kBlock + threadIdx.x;
+      ok[u] = idx[u] < nvec2;
+    }
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u][k] = ok[u] ? __builtin_nontemporal_load(reinterpret_cast<const d2*>(f.src[k]) + idx[u]) : d2{0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      d2 y;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double w = v[u][0][c];
+        int j = 1;
+        if constexpr (STEP0F32) {  // both operands fp32 arrays in the reference: fp32 subtraction
+          const float d = (float)v[u][1][c] - (float)w;
+          w = w + f.a[1] * (double)d;
+          j = 2;
+        }
+#pragma unroll
+        for (int k = 1; k <= N; ++k) {
+          if (k < j) continue;
+          if constexpr (RULE == CFA_RULE_SEQUENTIAL) w = w + f.a[k] * (v[u][k][c] - w);
+          else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV) w = w + (f.a[k] * (v[u][k][c] - w)) / f.d[k];
+          else w = w + f.a[k] * v[u][k][c];
+        }
+        if (compress) {
+          const long long e = 2 * idx[u] + c;
+          if (e >= cp.cbegin && e < cp.cend) w = compress_one_d(w, ref[e], cp, kept);
+        }
+        y[c] = w;
+      }
+      __builtin_nontemporal_store(y, reinterpret_cast<d2*>(out) + idx[u]);
+    }
+  }
+  if (compress) block_add_count(kept, cp.kept);
+}
+
+template <int RULE, bool STEP0F32>
+static void launch_fold_vec(int m, unsigned grid, hipStream_t st, double* out, const F64Fanin& f,
+                            long long nvec2, const double* ref, const CompressParams& cp, int compress) {
+#define CFA_CASE(K) \
+  case K:           \
+    fold_f64_vec_kernel<K, RULE, STEP0F32><<<grid, kBlock, 0, st>>>(out, f, nvec2, ref, cp, compress); \
+    break;
+  switch (m) {
+    CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6) CFA_CASE(7)
+    CFA_CASE(8) CFA_CASE(9) CFA_CASE(10) CFA_CASE(11) CFA_CASE(12) CFA_CASE(13) CFA_CASE(14)
+    CFA_CASE(15) CFA_CASE(16)
+    default: break;
+  }
+#undef CFA_CASE
+}
+
 struct MewmaF64Args {
   double* W;
   double* s[CFA_MAX_FANIN];
@@ -180,6 +255,61 @@ __global__ __launch_bounds__(kBlock) void mewma_tf1_f64_kernel(MewmaF64Args a, l
     }
     a.W[i] = W;
   }
+}
+
+// Vector form for unit-stride, 16-byte-aligned buckets: two doubles per lane, the fan-in N at
+// compile time so that every W / g / s load is issued before the first update.
+template <int N>
+__global__ __launch_bounds__(kBlock) void mewma_tf1_f64_vec_kernel(MewmaF64Args a, long long nvec2) {
+  const bool s32 = a.mask & CFA_TF1_STATE_F32, g32 = a.mask & CFA_TF1_GRAD_F32;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec2;
+       i += (long long)gridDim.x * kBlock) {
+    d2 Wv = __builtin_nontemporal_load(reinterpret_cast<const d2*>(a.W) + i);
+    d2 g[N], so[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      g[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(a.g[j]) + i);
+      if (!a.init) so[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(a.s[j]) + i);
+    }
+    d2 sn[N];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      double W = Wv[c];
+      bool w32 = a.mask & CFA_TF1_W_F32;
+      const double lr = 2 * i + c < a.split ? a.lr1 : a.lr2;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        double sv;
+        if (a.init) {
+          sv = g[j][c];
+        } else {
+          const double t1 = scale(a.rho, g[j][c], g32);
+          const double t2 = scale(a.one_minus_rho, so[j][c], s32);
+          sv = (g32 && s32) ? (double)((float)t1 + (float)t2) : t1 + t2;
+        }
+        if (s32) sv = (double)(float)sv;
+        sn[j][c] = sv;
+        const bool u32 = a.filtered ? s32 : g32;
+        const double t = scale(lr, a.filtered ? sv : g[j][c], u32);
+        if (w32 && u32) {
+          W = (double)((float)W - (float)t);
+        } else {
+          W = W - t;
+          w32 = false;
+        }
+      }
+      Wv[c] = W;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) __builtin_nontemporal_store(sn[j], reinterpret_cast<d2*>(a.s[j]) + i);
+    __builtin_nontemporal_store(Wv, reinterpret_cast<d2*>(a.W) + i);
+  }
+}
+
+template <int... Ns>
+static void launch_mewma_f64_vec(int m, unsigned grid, hipStream_t st, const MewmaF64Args& a, long long nvec2,
+                                 std::integer_sequence<int, Ns...>) {
+  ((m == Ns + 1 ? (void)(mewma_tf1_f64_vec_kernel<Ns + 1><<<grid, kBlock, 0, st>>>(a, nvec2)) : (void)0), ...);
 }
 
 template <bool FROM64, bool TO64>
@@ -343,10 +473,35 @@ int fold_f64(double* out, const double* local, const double* const* nbrs, const 
       f.a[j + 1] = alphas[done + j];
       f.d[j + 1] = divisors ? divisors[done + j] : 1.0;
     }
-    mix_tf1_f64_kernel<<<grid, kBlock, 0, st>>>(out, f, (long long)P, rule,
-                                                done == 0 ? step0_f32 : 0, local, cp,
-                                                last ? compress : 0);
-    if (int rc = check_launch("fold_f64")) return rc;
+    const int s0 = done == 0 ? step0_f32 : 0;
+    const int cmp = last ? compress : 0;
+    bool aligned = m >= 1 && (addr(out) & 15) == 0 && (addr(w) & 15) == 0 && (!cmp || (addr(local) & 15) == 0);
+    for (int j = 1; j <= m; ++j) aligned = aligned && (addr(f.src[j]) & 15) == 0;
+    long long nvec2 = aligned ? (long long)P / 2 : 0;
+    if (nvec2 > 0) {  // 16-byte body on the vector kernel, the odd last element on the scalar one
+      const long long tiles = (nvec2 + 2LL * kBlock - 1) / (2LL * kBlock);
+      const unsigned vgrid = grid_for(tiles);
+      if (rule == CFA_RULE_SEQUENTIAL && s0)
+        launch_fold_vec<CFA_RULE_SEQUENTIAL, true>(m, vgrid, st, out, f, nvec2, local, cp, cmp);
+      else if (rule == CFA_RULE_SEQUENTIAL)
+        launch_fold_vec<CFA_RULE_SEQUENTIAL, false>(m, vgrid, st, out, f, nvec2, local, cp, cmp);
+      else if (rule == CFA_RULE_SEQUENTIAL_DIV)
+        launch_fold_vec<CFA_RULE_SEQUENTIAL_DIV, false>(m, vgrid, st, out, f, nvec2, local, cp, cmp);
+      else
+        launch_fold_vec<CFA_RULE_ACCUMULATE, false>(m, vgrid, st, out, f, nvec2, local, cp, cmp);
+      if (int rc = check_launch("fold_f64_vec")) return rc;
+    }
+    const long long b = 2 * nvec2;
+    if (b < (long long)P) {
+      F64Fanin ft = f;
+      for (int j = 0; j <= m; ++j) ft.src[j] = f.src[j] + b;
+      CompressParams ct = cp;
+      ct.cbegin = cp.cbegin - b;
+      ct.cend = cp.cend - b;
+      mix_tf1_f64_kernel<<<b ? 1u : grid, kBlock, 0, st>>>(out + b, ft, (long long)P - b, rule, s0, local + b, ct,
+                                                          cmp);
+      if (int rc = check_launch("fold_f64")) return rc;
+    }
     done += m;
     w = out;
   } while (done < n);
@@ -401,9 +556,28 @@ extern "C" int cfa_mewma_tf1_f64(double* W, double* const* s, const double* cons
     a.init = init;
     a.filtered = use_filtered;
     a.mask = f32_mask;
-    mewma_tf1_f64_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
-        a, (long long)P);
-    if (int rc = check_launch("mewma_tf1_f64")) return rc;
+    bool vec = (addr(W) & 15) == 0;
+    for (int j = 0; j < m; ++j)
+      vec = vec && a.gstride[j] == 1 && (addr(a.s[j]) & 15) == 0 && (addr(a.g[j]) & 15) == 0;
+    const long long nvec2 = vec ? (long long)P / 2 : 0;
+    if (nvec2 > 0) {
+      launch_mewma_f64_vec(m, grid_for((nvec2 + kBlock - 1) / kBlock), st, a, nvec2,
+                           std::make_integer_sequence<int, CFA_MAX_FANIN>{});
+      if (int rc = check_launch("mewma_tf1_f64_vec")) return rc;
+    }
+    if (2 * nvec2 < (long long)P) {  // unaligned / strided buckets, or the odd last element
+      MewmaF64Args t = a;
+      const long long b = 2 * nvec2;
+      t.W = a.W + b;
+      for (int j = 0; j < m; ++j) {
+        t.s[j] = a.s[j] + b;
+        t.g[j] = a.g[j] + b * a.gstride[j];
+      }
+      t.split = a.split - b;
+      mewma_tf1_f64_kernel<<<grid_for(((long long)P - b + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+          t, (long long)P - b);
+      if (int rc = check_launch("mewma_tf1_f64")) return rc;
+    }
     done += m;
   }
   return CFA_OK;
