@@ -112,24 +112,38 @@ def open_transport(kind, rank, world, device):
     import torch.distributed as dist
     from federated_amd.dist import TorchTransport, make_transport
     import torch
+
+    def agree(ok: int) -> bool:  # every rank takes the same decision (MIN over the gloo group)
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag.item()) == 1
+
     t, ok = None, 1
     try:
         t = make_transport(kind, rank, world, device)
     except Exception as exc:
         ok = 0
         print(f"[bench rank {rank}] {kind} transport failed ({exc})", file=sys.stderr)
-    flag = torch.tensor([ok], dtype=torch.int32)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank takes the same decision
-    if int(flag.item()) == 1:
+    if agree(ok):
         return t
     if t is not None:
         t.close()
+    # torch P2P over an nccl (= RCCL) group: its communicator is created lazily, so probe it with
+    # one all-reduce before trusting it
+    ok, group = 1, None
     try:
-        t = TorchTransport(dist.new_group(backend="nccl"))
+        group = dist.new_group(backend="nccl")
+        probe = torch.ones(1, device=torch.device("cuda", device))
+        dist.all_reduce(probe, group=group)
+        torch.cuda.synchronize()
+        ok = int(float(probe.item()) == float(world))
+    except Exception as exc:
+        ok = 0
+        print(f"[bench rank {rank}] torch nccl group failed ({exc}); using gloo", file=sys.stderr)
+    if agree(ok):
+        t = TorchTransport(group)
         t.name = "torch-nccl"
         return t
-    except Exception as exc:
-        print(f"[bench rank {rank}] torch nccl group failed ({exc}); using gloo", file=sys.stderr)
     t = TorchTransport()
     t.name = "torch-gloo"
     return t
