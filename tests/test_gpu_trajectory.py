@@ -1,0 +1,81 @@
+"""Whole-run trajectories: R consensus rounds of a simulated population run two
+ways must agree bit for bit at every round:
+
+* the reference's way: every device calls the TF2 drop-in ``CFA_process.federated_weights_computing``
+  (consensus_v3.py:73-159 / consensus_v4.py:176-217) through the file protocol, reading its
+  neighbours' previous-round models from ``results/dump_train_model{k}.npy``;
+* the device-resident way: one ``topology.PopulationRound`` launch per round over the [D, P]
+  stack, with the same neighbour lists and eps policy (eps = 1/(n+1)).
+
+The per-device drop-in is itself pinned to the reference's outputs (test_gpu_consensus_golden),
+so this extends that parity from one call to whole multi-round runs.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# VGG-1-like layer list, scaled down (CIFAR-100 driver order: conv W, b, conv W, b, dense W, b)
+SHAPES = [(3, 3, 3, 8), (8,), (3, 3, 8, 8), (8,), (128, 10), (10,)]
+
+
+@pytest.fixture
+def workdir(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("FEDERATED_AMD_PAUSE_SCALE", "0")
+    os.makedirs("results")
+    return tmp_path
+
+
+def _obj(layers):
+    a = np.empty(len(layers), dtype=object)
+    for i, l in enumerate(layers):
+        a[i] = l
+    return a
+
+
+@pytest.mark.parametrize("version,N,D", [("v3", 2, 8), ("v3", 4, 9), ("v4", 1, 8)])
+def test_population_rounds_reproduce_dropin_trajectory(gpu, workdir, version, N, D):
+    from federated_amd import topology as T
+    if version == "v3":
+        from federated_amd.consensus.consensus_v3 import CFA_process
+        lists = T.kregular_v3(D, N)
+    else:
+        from federated_amd.consensus.consensus_v4 import CFA_process
+        lists = T.ring_v4(D, N)
+    rng = np.random.default_rng(D * 10 + N)
+    models = [[rng.standard_normal(s).astype(np.float32) for s in SHAPES] for _ in range(D)]
+    sizes = [int(np.prod(s)) for s in SHAPES]
+    flat = np.stack([np.concatenate([a.reshape(-1) for a in m]) for m in models])
+    pr = T.PopulationRound(gpu, torch.from_numpy(flat).cuda())
+    pr.set_topology(lists, T.alphas_tf2, use_window=False)
+    procs = [CFA_process(D, d, N) for d in range(D)]
+    for rnd in range(3):
+        # the reference way: every device publishes, then every device mixes its neighbours' files
+        for d in range(D):
+            np.save(f"results/dump_train_model{d}.npy", _obj(models[d]), allow_pickle=True)
+            np.savez(f"results/dump_train_variables{d}.npz", frame_count=rnd, epoch_count=rnd,
+                     training_end=False, loss=0.5)
+        new = []
+        for d in range(D):
+            p = procs[d]
+            p.update_local_model(_obj([a.copy() for a in models[d]]))
+            nb = lists[d]
+            if version == "v4" and N < 2:
+                out = p.federated_weights_computing(nb[0], N, rnd, 0.5, 0, 30)
+            else:
+                out = p.federated_weights_computing(np.asarray(nb), N, rnd, 0.5, 0, 30)
+            new.append([np.asarray(a, dtype=np.float32) for a in out])
+        models = new
+        # the device-resident way: one launch for the population
+        out = pr.run()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for d in range(D):
+            ref = np.concatenate([a.reshape(-1) for a in models[d]])
+            assert np.array_equal(got[d], ref), (version, rnd, d)
+        pr.models.copy_(out)
+    assert sum(sizes) == flat.shape[1]
