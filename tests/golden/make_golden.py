@@ -449,6 +449,72 @@ def case_tf2():
     save("tf2_consensus.npz", **out)
 
 
+def case_variants():
+    """Copies not covered above: TF1 cfa_mobilenet.py over several epochs of the vGraph mobile
+    network; the CIFAR100 consensus_v3_threading.py (mixing under a caller lock); the
+    FL_over_MQTT consensus_v3.py, whose constructor reads an undefined global `devices`
+    (NameError as shipped; run here with that global injected to record its outputs)."""
+    import threading
+    out = {}
+    # -- cfa_mobilenet: 5 devices (vGraph is 5 x 5 x 111), epochs 0..3, every device each epoch
+    mn = load_ref(os.path.join(TF1, "consensus", "cfa_mobilenet.py"), "ref_tf1_cfa_mn")
+    K, N, eps = 5, 2, 0.8
+    rng = np.random.default_rng(4242)
+    epochs = 4
+    locals_ = [[gen_model(rng, SHAPES_CNN_GE) for _ in range(K)] for _ in range(epochs)]
+    for e in range(epochs):
+        for t in range(4):
+            out[f"mobilenet/local_e{e}_{t}"] = np.stack([m[t] for m in locals_[e]])
+    out["mobilenet/meta"] = np.array([K, N, epochs], dtype=np.int64)
+    out["mobilenet/eps"] = np.array(eps)
+    with Workdir():
+        procs = [mn.CFA_process(True, K, j, N) for j in range(K)]
+        for e in range(epochs):
+            for j in range(K):
+                W1, b1, W2, b2 = locals_[e][j]
+                res = procs[j].getFederatedWeight(W1, W2, b1, b2, e, np.zeros(3), eps)
+                if e > 0:
+                    out[f"mobilenet/nbr_e{e}_{j}"] = np.asarray(procs[j].neighbor_vec, dtype=np.int64)
+                for t in range(4):
+                    out[f"mobilenet/out_e{e}_{j}_{t}"] = np.asarray(res[t])
+    # -- TF2 copies: the same published population and local model as case_tf2's layer list
+    D = 6
+    rng = np.random.default_rng(5151)
+    models = [gen_model(rng, SHAPES_LENET1) for _ in range(D)]
+    local = gen_model(rng, SHAPES_LENET1)
+    for t in range(len(SHAPES_LENET1)):
+        out[f"tf2/models_{t}"] = np.stack([m[t] for m in models])
+        out[f"tf2/local_{t}"] = local[t]
+    thr = load_ref(os.path.join(TF2, "CIFAR100_dataset", "consensus", "consensus_v3_threading.py"), "ref_tf2_v3t")
+    mq = load_ref(os.path.join(TF2, "FL_over_MQTT", "consensus", "consensus_v3.py"), "ref_tf2_v3mqtt")
+    try:
+        mq.CFA_process(0, 2)
+        out["mqtt/ctor_raises_nameerror"] = np.array(False)
+    except NameError:
+        out["mqtt/ctor_raises_nameerror"] = np.array(True)
+    mq.devices = D  # the global the shipped constructor expects
+    cases = [("threading_n3", "thr", [1, 3, 5], 3, ()), ("threading_end", "thr", [2, 4], 2, (4,)),
+             ("mqtt_n2", "mq", [4, 5], 2, ()), ("mqtt_end", "mq", [1, 2, 3], 3, (1,))]
+    out["tf2/cases"] = np.array([c[0] for c in cases])
+    for tag, which, nbr, nnb, ended in cases:
+        with Workdir():
+            for k in range(D):
+                publish_tf2(k, models[k], 10, k in ended)
+            p = thr.CFA_process(threading.Lock(), D, 0, 2) if which == "thr" else mq.CFA_process(0, 2)
+            np.random.seed(321)
+            loc = obj_array([a.copy() for a in local])
+            p.update_local_model(loc)
+            res = p.federated_weights_computing(nbr, nnb, 10, 0.5, 0, 30)
+            probe = np.random.random()
+        out[f"tf2/{tag}/nbr"] = np.asarray(nbr, dtype=np.int64)
+        out[f"tf2/{tag}/ended"] = np.array(ended, dtype=np.int64)
+        out[f"tf2/{tag}/rng_probe"] = np.array(probe)
+        for t in range(len(SHAPES_LENET1)):
+            out[f"tf2/{tag}/out_{t}"] = np.asarray(res[t])
+            out[f"tf2/{tag}/inplace_{t}"] = np.asarray(loc[t])
+    save("variants.npz", **out)
+
+
 def case_topology():
     cfa = load_ref(os.path.join(TF1, "consensus", "cfa.py"), "ref_tf1_cfa_topo")
     v3 = load_v3()
@@ -695,6 +761,7 @@ def main():
     case_tf2()
     case_parameter_server()
     case_driver_aggregations()
+    case_variants()
 
 
 if __name__ == "__main__":
