@@ -493,20 +493,30 @@ def case_variants():
     except NameError:
         out["mqtt/ctor_raises_nameerror"] = np.array(True)
     mq.devices = D  # the global the shipped constructor expects
+    rv4 = load_ref(os.path.join(TF2, "FL_radar_dataset", "consensus", "consensus_v4.py"), "ref_tf2_v4radar")
     cases = [("threading_n3", "thr", [1, 3, 5], 3, ()), ("threading_end", "thr", [2, 4], 2, (4,)),
-             ("mqtt_n2", "mq", [4, 5], 2, ()), ("mqtt_end", "mq", [1, 2, 3], 3, (1,))]
+             ("mqtt_n2", "mq", [4, 5], 2, ()), ("mqtt_end", "mq", [1, 2, 3], 3, (1,)),
+             # FL_radar v4: one neighbour id, read `neighbors` times (consensus_v4.py:88-89)
+             ("radar_v4_n1", "rv4", 3, 1, ()), ("radar_v4_n2", "rv4", 5, 2, ()),
+             ("radar_v4_end", "rv4", 2, 2, (2,))]
     out["tf2/cases"] = np.array([c[0] for c in cases])
     for tag, which, nbr, nnb, ended in cases:
         with Workdir():
             for k in range(D):
                 publish_tf2(k, models[k], 10, k in ended)
-            p = thr.CFA_process(threading.Lock(), D, 0, 2) if which == "thr" else mq.CFA_process(0, 2)
+            if which == "thr":
+                p = thr.CFA_process(threading.Lock(), D, 0, 2)
+            elif which == "mq":
+                p = mq.CFA_process(0, 2)
+            else:
+                p = rv4.CFA_process(D, 0, 1)
             np.random.seed(321)
             loc = obj_array([a.copy() for a in local])
             p.update_local_model(loc)
             res = p.federated_weights_computing(nbr, nnb, 10, 0.5, 0, 30)
             probe = np.random.random()
         out[f"tf2/{tag}/nbr"] = np.asarray(nbr, dtype=np.int64)
+        out[f"tf2/{tag}/nnb"] = np.array(nnb, dtype=np.int64)
         out[f"tf2/{tag}/ended"] = np.array(ended, dtype=np.int64)
         out[f"tf2/{tag}/rng_probe"] = np.array(probe)
         for t in range(len(SHAPES_LENET1)):

@@ -6,7 +6,9 @@
   bit for bit;
 * CIFAR-100 ``consensus_v3_threading.py``: the mix under the caller's lock;
 * FL_over_MQTT ``consensus_v3.py``: its constructor raises NameError as shipped (checked on the
-  CPU); with ``devices`` supplied the outputs equal the reference's run with the global injected.
+  CPU); with ``devices`` supplied the outputs equal the reference's run with the global injected;
+* FL_radar ``consensus_v4.py``: one neighbour id read ``neighbors`` times (its lines 86-89),
+  including the transfer-learning branch when that neighbour has ended.
 """
 import os
 import threading
@@ -67,7 +69,8 @@ def test_cfa_mobilenet_epochs(gpu, workdir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["threading_n3", "threading_end", "mqtt_n2", "mqtt_end"])
+@pytest.mark.parametrize("tag", ["threading_n3", "threading_end", "mqtt_n2", "mqtt_end",
+                                 "radar_v4_n1", "radar_v4_n2", "radar_v4_end"])
 def test_tf2_copies(gpu, workdir, tag):
     z = load_golden("variants.npz")
     D = z["tf2/models_0"].shape[0]
@@ -81,14 +84,18 @@ def test_tf2_copies(gpu, workdir, tag):
     if tag.startswith("threading"):
         from federated_amd.consensus.consensus_v3_threading import CFA_process
         p = CFA_process(threading.Lock(), D, 0, 2)
+    elif tag.startswith("radar_v4"):
+        from federated_amd.consensus.fl_radar.consensus_v4 import CFA_process
+        p = CFA_process(D, 0, 1)
     else:
         from federated_amd.consensus.fl_over_mqtt.consensus_v3 import CFA_process
         p = CFA_process(0, 2, devices=D)
     nbr = z[f"tf2/{tag}/nbr"].tolist()
+    nnb = int(z[f"tf2/{tag}/nnb"])
     np.random.seed(321)
     loc = _obj([a.copy() for a in local])
     p.update_local_model(loc)
-    res = p.federated_weights_computing(nbr, len(nbr), 10, 0.5, 0, 30)
+    res = p.federated_weights_computing(nbr, nnb, 10, 0.5, 0, 30)
     assert np.random.random() == float(z[f"tf2/{tag}/rng_probe"])
     for t in range(L2):
         ref = z[f"tf2/{tag}/out_{t}"]

@@ -142,6 +142,31 @@ def test_tf2_consensus_oracle_bitexact():
         assert bool(z[f"{tag}/meta"][1]) == end
 
 
+def test_tf2_variant_copies_oracle_bitexact():
+    """variants.npz: CIFAR-100 v3_threading, FL_over_MQTT v3 and FL_radar v4 (one neighbour id
+    read ``neighbors`` times, FL_radar_dataset/consensus/consensus_v4.py:86-89) all reduce to the
+    same weight rule (tf2_weights)."""
+    z = load_golden("variants.npz")
+    L = 6
+    models = [[z[f"tf2/models_{t}"][d] for t in range(L)] for d in range(z["tf2/models_0"].shape[0])]
+    local = [z[f"tf2/local_{t}"] for t in range(L)]
+    for tag in (str(t) for t in z["tf2/cases"]):
+        nbr = np.atleast_1d(z[f"tf2/{tag}/nbr"]).tolist()
+        if tag.startswith("radar_v4"):
+            nbr = nbr * int(z[f"tf2/{tag}/nnb"])
+        ended = set(z[f"tf2/{tag}/ended"].tolist())
+        loaded, end = [], False
+        for j in nbr:
+            loaded.append(j)
+            end = j in ended
+            if end:
+                break
+        out = O.tf2_weights(local, [models[j] for j in loaded], training_end=end)
+        for t in range(L):
+            ref = z[f"tf2/{tag}/out_{t}"]
+            assert out[t].dtype == ref.dtype and np.array_equal(out[t], ref), (tag, t)
+
+
 def test_closed_form_equals_sequential_in_exact_arithmetic():
     from fractions import Fraction
     alphas = [Fraction(1, 3), Fraction(1, 3), Fraction(2, 7)]
