@@ -28,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from ._graphs import RoundGraphs
 from .consensus import _tf1
 from .engine import Engine
 
@@ -116,6 +117,7 @@ class CfaGePopulation:
             dst = torch.tensor([mixed[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
             self._tables.append((src, dst))
         self._bufs, self._rot = bufs, 0
+        self._graphs: Optional[RoundGraphs] = None  # captured periods hold these tables
         states, grads = [], ([], [])
         for i, nb in enumerate(self.lists):
             states.append(0)
@@ -162,6 +164,19 @@ class CfaGePopulation:
         self.W, self.pub, self.mixed = b[self._rot], b[(self._rot + 1) % 3], b[(self._rot + 2) % 3]
         self.G, self.G_next = self.G_next, self.G
         self._gpar ^= 1
+
+    def rounds(self, R: int, graph: bool = True) -> None:
+        """R consecutive ``round()`` calls on the current stream. ``graph=True`` replays
+        captured 6-round periods (the (W, pub, mixed) rotation times the (G, G_next) swap
+        returns to its start after 6 rounds) as hipGraphs, so a round costs its kernels and not
+        its Python launch path; the results equal R eager rounds bit for bit."""
+        if not graph:
+            for _ in range(R):
+                self.round()
+            return
+        if self._graphs is None:
+            self._graphs = RoundGraphs(self.engine.device, self.round, 6, lambda: (self._rot, self._gpar))
+        self._graphs.run(R)
 
     @property
     def bytes_per_round(self) -> int:

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from .consensus import _tf1, _tf2
+from ._graphs import RoundGraphs
 from .engine import Engine
 
 RULE_SEQUENTIAL = 0
@@ -127,6 +128,8 @@ class PopulationRound:
         self.dst = torch.tensor([self.out[d].data_ptr() for d in range(D)], dtype=torch.int64, device=dev)
         self.tables = None
         self.window = None  # (hl, hr, per-device alphas) when the topology is a ring window
+        self._graphs: Optional[RoundGraphs] = None  # captured rounds, rebuilt per topology
+        self._parity = 0
 
     def set_topology(self, lists, policy, use_window: Optional[bool] = None) -> None:
         """CSR tables for the one-launch population kernel. A ring-window topology with one
@@ -144,17 +147,53 @@ class PopulationRound:
         alphas = [list(policy(nb, d, D)) for d, nb in enumerate(lists)]
         shape = window_shape(lists, alphas) if use_window else None
         self.window = (shape[0], shape[1], alphas) if shape else None
+        self._graphs = None
 
     def run(self, stream=None) -> torch.Tensor:
+        """One round: every device's mix of ``models`` into ``out``."""
+        self._launch(self.models, self.out, self.src, self.dst, stream)
+        return self.out
+
+    def _launch(self, models, out, src, dst, stream=None) -> None:
         if self.tables is None:
             raise RuntimeError("set_topology() first")
-        D, P = self.models.shape
+        D, P = models.shape
         if self.window is not None:
             hl, hr, alphas = self.window
             for s in range(0, D, 8):
                 devs = list(range(s, min(s + 8, D)))
-                rows = [self.models[(s + o) % D] for o in range(-hl, len(devs) + hr)]
-                self.engine.mix_window([self.out[d] for d in devs], rows, [alphas[d] for d in devs], hl, hr, stream)
-            return self.out
-        self.engine.population(self.dst, self.src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
-        return self.out
+                rows = [models[(s + o) % D] for o in range(-hl, len(devs) + hr)]
+                self.engine.mix_window([out[d] for d in devs], rows, [alphas[d] for d in devs], hl, hr, stream)
+            return
+        self.engine.population(dst, src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
+
+    def rounds(self, R: int, graph: bool = True) -> torch.Tensor:
+        """R consecutive rounds on the current stream, each mixing the previous round's output
+        (the per-device reference run, repeated: every device's round r reads its neighbours'
+        round r-1 models). ``models`` and ``out`` alternate as source and destination; the
+        result is left in ``models`` (one extra copy when R is odd) and returned.
+        ``graph=True`` replays captured pairs of rounds (hipGraph) instead of launching each
+        round from Python; the results are the same bit for bit."""
+        if R <= 0:
+            return self.models
+        if not graph:
+            for r in range(R):
+                self._step_pair(r & 1)
+        else:
+            if self._graphs is None:
+                self._graphs = RoundGraphs(self.models.device, self._graph_step, 2, lambda: self._parity)
+            self._parity = 0
+            self._graphs.run(R)
+        if R & 1:
+            self.models.copy_(self.out)
+        return self.models
+
+    def _step_pair(self, parity: int) -> None:
+        if parity == 0:
+            self._launch(self.models, self.out, self.src, self.dst)
+        else:
+            self._launch(self.out, self.models, self.dst, self.src)
+
+    def _graph_step(self) -> None:
+        self._step_pair(self._parity)
+        self._parity ^= 1

@@ -1,0 +1,79 @@
+"""Graph-replayed rounds (federated_amd/_graphs.py) equal eager rounds bit for bit.
+
+``PopulationRound.rounds`` and ``CfaGePopulation.rounds`` capture whole periods of their buffer
+rotation as hipGraphs. The graphs must hold the same kernels with the same arguments as the
+eager rounds, for every starting phase and for round counts that leave partial periods."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("D,P,use_window,lists_kind", [(16, 1488, False, "kreg"), (9, 4100, True, "ring"),
+                                                      (12, 777, False, "kreg")])
+@pytest.mark.parametrize("R", [1, 2, 5, 19])
+def test_population_rounds_graph_equals_eager(gpu, D, P, use_window, lists_kind, R):
+    from federated_amd import topology as T
+    if lists_kind == "kreg":
+        lists = T.kregular_v3(D, 2)
+    else:  # ring window [d-1, d+1, d+2] (hl 1, hr 2): the window-pass path
+        lists = [[(d - 1) % D, (d + 1) % D, (d + 2) % D] for d in range(D)]
+    g = torch.Generator(device="cuda").manual_seed(D * 100 + P)
+    m0 = torch.randn(D, P, device="cuda", generator=g)
+    ref = m0.clone()
+    pr_ref = T.PopulationRound(gpu, ref)
+    pr_ref.set_topology(lists, T.alphas_tf2, use_window=use_window)
+    for _ in range(R):
+        pr_ref.run()
+        ref.copy_(pr_ref.out)
+    got = m0.clone()
+    pr = T.PopulationRound(gpu, got)
+    pr.set_topology(lists, T.alphas_tf2, use_window=use_window)
+    assert (pr.window is not None) == use_window
+    out = pr.rounds(R)
+    assert out is got
+    # a second call starts from the result of the first (reuses the captured graphs)
+    pr.rounds(R)
+    for _ in range(R):
+        pr_ref.run()
+        ref.copy_(pr_ref.out)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    eager = m0.clone()
+    pe = T.PopulationRound(gpu, eager)
+    pe.set_topology(lists, T.alphas_tf2, use_window=use_window)
+    pe.rounds(2 * R, graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(eager, ref)
+
+
+def _ge_pop(gpu, ml, D, N, seed):
+    from federated_amd import topology
+    from federated_amd.cfa_ge_population import CfaGePopulation
+    geom = {"filter": 16, "number": 8, "stride": 5} if ml == 1 else {"intermediate_nodes": 32}
+    rng = np.random.default_rng(seed)
+    B, L, C = 24, 512, 8
+    x = torch.from_numpy(rng.standard_normal((D, B, L)).astype(np.float32)).cuda()
+    y = torch.from_numpy(np.eye(C, dtype=np.float32)[rng.integers(0, C, (D, B))]).cuda()
+    pop = CfaGePopulation(gpu, ml, geom, x, y, topology.kregular_tf1(D, N), 1.0, N, 0.99, 0.1, 0.1)
+    W = torch.from_numpy((rng.standard_normal((D, pop.P)) * 0.1).astype(np.float32)).cuda()
+    pop.load(W, W.clone())
+    return pop
+
+
+@pytest.mark.parametrize("ml", [1, 2])
+@pytest.mark.parametrize("pre,R", [(0, 6), (0, 13), (2, 50), (5, 7)])
+def test_cfa_ge_rounds_graph_equals_eager(gpu, ml, pre, R):
+    a = _ge_pop(gpu, ml, 16, 2, 7)
+    b = _ge_pop(gpu, ml, 16, 2, 7)
+    for _ in range(pre):  # start the graph at another phase of the 6-round period
+        a.round()
+        b.round()
+    a.rounds(R, graph=False)
+    b.rounds(R)
+    b.rounds(3)
+    a.rounds(3, graph=False)
+    torch.cuda.synchronize()
+    for name in ("W", "pub", "S", "G"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name

@@ -96,6 +96,16 @@ def population(D, P, lists, policy, reps=20, use_window=None):
     e1.record()
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / reps * 1e-3
+    # R rounds replayed from captured hipGraphs (PopulationRound.rounds): kernels only, no
+    # per-round Python launch path (the eager loop above also pays no copy: it re-mixes models)
+    R = 10 * reps
+    pr.rounds(R)
+    torch.cuda.synchronize()
+    e0.record()
+    pr.rounds(R)
+    e1.record()
+    torch.cuda.synchronize()
+    t_graph = e0.elapsed_time(e1) / R * 1e-3
     B = sum((len(l) + 2) * P * 4 for l in lists)
     host = models.cpu().numpy()
 
@@ -104,7 +114,8 @@ def population(D, P, lists, policy, reps=20, use_window=None):
             O.sequential_mix(host[d], [host[j] for j in lists[d]], policy(lists[d], d, D))
     t_np = med_time(numpy_round, 2)
     return {"devices": D, "P": P, "path": "window" if pr.window else "csr", "round_us": round(t * 1e6, 1),
-            "GBps": round(B / t / 1e9, 1),
+            "GBps": round(B / t / 1e9, 1), "round_us_graph": round(t_graph * 1e6, 2),
+            "GBps_graph": round(B / t_graph / 1e9, 1),
             "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
 
 
@@ -165,6 +176,17 @@ def cfa_ge_population(D=16, N=2, B=24, ml=1, rounds=50):
     torch.cuda.synchronize()
     host_us = (time.perf_counter() - t0) / rounds * 1e6
     gpu_us = e0.elapsed_time(e1) / rounds * 1e3
+    # the same rounds replayed from captured 6-round hipGraphs (CfaGePopulation.rounds)
+    R = 48 * 10
+    pop.rounds(R)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    pop.rounds(R)
+    e1.record()
+    torch.cuda.synchronize()
+    graph_host_us = (time.perf_counter() - t0) / R * 1e6
+    graph_us = e0.elapsed_time(e1) / R * 1e3
     Nm = max(len(l) for l in lists)
     Wd = W.astype(np.float64)
     G = np.zeros((D, Nm, P))
@@ -172,7 +194,9 @@ def cfa_ge_population(D=16, N=2, B=24, ml=1, rounds=50):
     t = med_time(lambda: O.cfa_ge_population_round(Wd, Wd, G, S, lists, x, y, ml, full, 1.0, N, 0.99, 0.1, 0.1), 3)
     return {"devices": D, "neighbours": N, "samples": B, "P": P, "model": "cnn" if ml == 1 else "2nn",
             "round_us_gpu_events": round(gpu_us, 1), "round_us_host": round(host_us, 1),
-            "numpy_round_ms_1core": round(t * 1e3, 2), "speedup_vs_numpy": round(t * 1e6 / host_us, 1)}
+            "round_us_graph": round(graph_us, 2), "round_us_graph_host": round(graph_host_us, 2),
+            "numpy_round_ms_1core": round(t * 1e3, 2), "speedup_vs_numpy": round(t * 1e6 / host_us, 1),
+            "speedup_vs_numpy_graph": round(t * 1e6 / graph_host_us, 1)}
 
 
 def main():
