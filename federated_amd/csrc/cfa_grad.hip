@@ -26,10 +26,16 @@ constexpr float kClipLo = 1e-15f, kClipHi = 0.99f;
 // Phase timestamps for tools/probe/grad_phases.hip (compiled out of the library).
 #ifdef CFA_GRAD_PHASES
 __device__ unsigned long long g_phase[32];
+__device__ unsigned long long g_wg[4096][2];  // per workgroup: first and last stamp
 #define PHASE(k) \
   do {           \
     __syncthreads(); \
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_phase[k] = wall_clock64(); \
+    if (threadIdx.x == 0) { \
+      const unsigned long long t_ = wall_clock64(); \
+      const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x; \
+      if (blockIdx.x == 0 && blockIdx.y == 0) g_phase[k] = t_; \
+      if (wg_ < 4096) g_wg[wg_][(k) == 0 || (k) == 10 ? 0 : 1] = t_; \
+    } \
   } while (0)
 #else
 #define PHASE(k) \
@@ -43,50 +49,85 @@ __host__ __device__ inline int same_left(int L, int k, int s) {
   return total / 2;
 }
 
-// Softmax + clipped cross-entropy backward for one sample: logits[C] in, dlogits[C] out (in place).
+// Softmax + clipped cross-entropy backward, in place on logits z[nb][C] -> d logits:
 // d cost / d pred_c = -(y_c / clip(pred_c)) / B where the clip passes the gradient; then the
-// softmax gradient (dp - sum(dp * p)) * p (TF SoftmaxGrad).
-__device__ void softmax_xent_backward(float* z, const float* y, int C, float invB) {
-  float mx = z[0];
-  for (int c = 1; c < C; ++c) mx = fmaxf(mx, z[c]);
-  float s = 0.f;
-  for (int c = 0; c < C; ++c) {
-    z[c] = expf(z[c] - mx);
-    s += z[c];
+// softmax gradient (dp - sum(dp * p)) * p (TF SoftmaxGrad). One lane per class: a sample's
+// W >= C lanes (W a power of two <= 64, so a group never straddles a wave) reduce max, sum and
+// dot with xor shuffles, and every value stays in registers.
+__device__ void softmax_xent_backward(float* z, const float* y, int nb, int C, int W, float invB, int tid,
+                                      int T) {
+  for (int idx = tid; idx < nb * W; idx += T) {
+    const int b = idx / W, c = idx % W;
+    const bool valid = c < C;
+    const float zc = valid ? z[b * C + c] : -INFINITY;
+    const float yc = valid ? y[b * C + c] : 0.f;
+    float mx = zc;
+    for (int o = W >> 1; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, W));
+    const float e = valid ? expf(zc - mx) : 0.f;
+    float s = e;
+    for (int o = W >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, W);
+    const float p = e / s;  // pred
+    const bool pass = valid && p >= kClipLo && p <= kClipHi;
+    const float dp = pass ? -(yc / fminf(fmaxf(p, kClipLo), kClipHi)) * invB : 0.f;
+    float dot = dp * p;
+    for (int o = W >> 1; o > 0; o >>= 1) dot += __shfl_xor(dot, o, W);
+    if (valid) z[b * C + c] = (dp - dot) * p;
   }
-  auto dpred = [&](float p, int c) {
-    const bool pass = p >= kClipLo && p <= kClipHi;
-    return pass ? -(y[c] / fminf(fmaxf(p, kClipLo), kClipHi)) * invB : 0.f;
-  };
-  float dot = 0.f;
-  for (int c = 0; c < C; ++c) {
-    z[c] = z[c] / s;  // pred
-    dot = fmaf(dpred(z[c], c), z[c], dot);
-  }
-  for (int c = 0; c < C; ++c) z[c] = (dpred(z[c], c) - dot) * z[c];
+}
+
+// lanes per sample of softmax_xent_backward: the power of two >= C (C <= 64, checked on the host)
+inline int softmax_width(int C) {
+  int w = 1;
+  while (w < C) w <<= 1;
+  return w;
 }
 
 constexpr int kGradBlock = 512;  // 8 waves: these graphs are latency-bound, not ALU-bound
 
 // Copy n floats global -> LDS with every load of a thread issued before its first store (the
-// graphs are tiny, so serialized global latency, not bandwidth, would dominate).
+// graphs are tiny, so serialized global latency, not bandwidth, would dominate). The tail is
+// predicated rather than looped, so a copy of up to U * T floats is one round trip.
 __device__ __forceinline__ void stage(float* dst, const float* src, int n, int tid, int T) {
   constexpr int U = 8;
-  int i = tid;
-  for (; i + (U - 1) * T < n; i += U * T) {
+  for (int i = tid; i < n; i += U * T) {
     float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = src[i + u * T];
+    for (int u = 0; u < U; ++u) v[u] = i + u * T < n ? src[i + u * T] : 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) dst[i + u * T] = v[u];
+    for (int u = 0; u < U; ++u)
+      if (i + u * T < n) dst[i + u * T] = v[u];
   }
-  for (; i < n; i += T) dst[i] = src[i];
+}
+
+// stage() of three segments with all their loads in flight together.
+__device__ __forceinline__ void stage3(float* d0, const float* s0, int n0, float* d1, const float* s1, int n1,
+                                       float* d2, const float* s2, int n2, int tid, int T) {
+  constexpr int U = 4;
+  const int n = max(n0, max(n1, n2));
+  for (int i = tid; i < n; i += U * T) {
+    float v0[U], v1[U], v2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = i + u * T;
+      v0[u] = j < n0 ? s0[j] : 0.f;
+      v1[u] = j < n1 ? s1[j] : 0.f;
+      v2[u] = j < n2 ? s2[j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = i + u * T;
+      if (j < n0) d0[j] = v0[u];
+      if (j < n1) d1[j] = v1[u];
+      if (j < n2) d2[j] = v2[u];
+    }
+  }
 }
 
 constexpr int kMaxTaps = 32;  // conv filter taps held in registers (larger filters read LDS)
 
 struct CnnDims {
   int B, L, C, F, NC, S;
+  int SW;              // softmax lanes per sample (softmax_width(C))
   int L1, L2, pl, ql;  // conv / pool output lengths, left pads
   int Bc;              // samples per LDS-resident chunk
   int Bs;              // samples per workgroup (grid.y splits the batch; partial sums go to a workspace)
@@ -147,7 +188,10 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   const float invB = 1.0f / (float)d.B;
 
   PHASE(0);
-  stage(W1, m, nG1 + nW2 + d.C, tid, T);  // model bucket = W1 b1 W2 b2
+  // the model bucket (W1 b1 W2 b2) and the first chunk's samples and labels, all in flight
+  // together: one global round trip before the first barrier
+  stage3(W1, m, nG1 + nW2 + d.C, xs, x + (long long)bb * d.L, bb < be ? min(d.Bc, be - bb) * d.L : 0, ys,
+         y + (long long)bb * d.C, bb < be ? min(d.Bc, be - bb) * d.C : 0, tid, T);
   __syncthreads();
   PHASE(1);
   // the conv taps of this thread's channel stay in registers (T is a multiple of NC, so every
@@ -163,9 +207,11 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   for (int b0 = bb; b0 < be; b0 += d.Bc) {
     const int nb = min(d.Bc, be - b0);
     const bool first = b0 == bb;
-    stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
-    stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
-    __syncthreads();
+    if (!first) {  // the first chunk was staged with the model
+      stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
+      stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
+      __syncthreads();
+    }
     PHASE(2);
     // conv + bias + relu evaluated inside each pooling window; keep the max and its position
     for (int idx = tid; idx < nb * LN; idx += T) {
@@ -239,7 +285,7 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
     }
     __syncthreads();
     PHASE(4);
-    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, ys + b * d.C, d.C, invB);
+    softmax_xent_backward(zl, ys, nb, d.C, d.SW, invB, tid, T);
     __syncthreads();
     PHASE(5);
 
@@ -301,6 +347,7 @@ constexpr int kSpan = 32;  // first-layer inputs per partial sum (W1 slice held 
 
 struct NnDims {
   int B, L, H, C;
+  int SW;  // softmax lanes per sample (softmax_width(C))
   int G;   // ceil(L / kSpan) slices of the input dimension for the first layer's partial sums
   int Bc;
   int Bs;  // samples per workgroup (grid.y splits the batch; partial sums go to a workspace)
@@ -345,9 +392,9 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
   const int H4 = (d.H % 4 == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0) ? d.H / 4 : 0;
 
   PHASE(10);
-  stage(b1, m + nW1, d.H + d.H * d.C + d.C, tid, T);
   // W1 slice of this thread's (slice, h) pairs: with G * H <= T every thread owns one pair and
-  // loads its kSpan weights once, all in flight together
+  // loads its kSpan weights once. These loads, the rest of the model (b1 W2 b2) and the first
+  // chunk's samples and labels are all in flight together: one global round trip.
   const bool w_in_regs = d.G * d.H <= T;
   float wreg[kSpan];
   {
@@ -356,6 +403,8 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
     for (int u = 0; u < kSpan; ++u)
       wreg[u] = (w_in_regs && grp < d.G && i0 + u < d.L) ? W1[(long long)(i0 + u) * d.H + h] : 0.f;
   }
+  stage3(b1, m + nW1, d.H + d.H * d.C + d.C, xs, x + (long long)bb * d.L, bb < be ? min(d.Bc, be - bb) * d.L : 0,
+         ys, y + (long long)bb * d.C, bb < be ? min(d.Bc, be - bb) * d.C : 0, tid, T);
   if (bb >= be) {  // no sample left for this split: a zero partial
     for (long long i = threadIdx.x; i < d.P; i += blockDim.x) g[i] = 0.f;
     return;
@@ -363,8 +412,10 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
   for (int b0 = bb; b0 < be; b0 += d.Bc) {
     const int nb = min(d.Bc, be - b0);
     const bool first = b0 == bb;
-    stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
-    stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
+    if (!first) {  // the first chunk was staged with the model
+      stage(xs, x + (long long)b0 * d.L, nb * d.L, tid, T);
+      stage(ys, y + (long long)b0 * d.C, nb * d.C, tid, T);
+    }
     __syncthreads();
     PHASE(11);
     // first layer as G partial sums over kSpan-wide slices of the input dimension
@@ -416,7 +467,7 @@ __global__ __launch_bounds__(kGradBlock) void grad_2nn_kernel(const float* __res
     }
     __syncthreads();
     PHASE(14);
-    for (int b = tid; b < nb; b += T) softmax_xent_backward(zl + b * d.C, ys + b * d.C, d.C, invB);
+    softmax_xent_backward(zl, ys, nb, d.C, d.SW, invB, tid, T);
     __syncthreads();
     PHASE(15);
     for (int idx = tid; idx < d.H * d.C; idx += T) {
@@ -552,6 +603,12 @@ __global__ __launch_bounds__(kBlock) void reduce_splits_kernel(const float* __re
   }
 }
 
+int launch_reduce_splits(const float* ws, float* grads, int M, int Sp, long long P, hipStream_t st) {
+  reduce_splits_kernel<<<dim3((unsigned)std::min<long long>((P + kBlock - 1) / kBlock, 64), (unsigned)M), kBlock, 0,
+                         st>>>(ws, grads, Sp, P);
+  return check_launch("reduce_splits_kernel");
+}
+
 // Batch split for M evaluations of B samples of P-parameter models: about two workgroups per CU
 // in all, at most 8 per evaluation, and fewer for larger models, whose partial buckets (written
 // and re-read by the reduction) and per-workgroup weight staging grow with P. Measured at the
@@ -567,6 +624,9 @@ int batch_split(int M, int B, long long P) {
   return (B + bs - 1) / bs;
 }
 
+// Workspace of a split launch: the M * Sp partial buckets.
+size_t split_workspace_elems(int M, int Sp, long long P) { return (size_t)M * Sp * (size_t)P; }
+
 int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L, int classes, int filter,
                     int number, int stride, const float* models, const int* mrow, const int* drow,
                     float* grads, float* ws, size_t ws_elems, int M, void* stream) {
@@ -576,7 +636,9 @@ int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L
   if (M == 0) return CFA_OK;
   if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   CnnDims d;
+  if (classes > 64) return fail(CFA_E_UNSUPPORTED, "%s: more than 64 classes", fn);
   d.B = B, d.L = L, d.C = classes, d.F = filter, d.NC = number, d.S = stride;
+  d.SW = softmax_width(classes);
   d.L1 = (L + stride - 1) / stride;
   d.L2 = (d.L1 + stride - 1) / stride;
   d.pl = same_left(L, filter, stride);
@@ -587,25 +649,21 @@ int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L
   // the unrolled kernel
   const bool fast = filter == 16 && stride == 5;
   const void* kern = fast ? (const void*)grad_cnn_kernel<16, 5> : (const void*)grad_cnn_kernel<0, 0>;
-  d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), B, &bytes);
-  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
   int Sp = batch_split(M, B, d.P);
-  if (!ws || ws_elems < (size_t)M * Sp * (size_t)d.P) Sp = 1;
+  if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) Sp = 1;
   d.Bs = (B + Sp - 1) / Sp;
-  float* out = Sp > 1 ? ws : grads;
+  // LDS for the samples one workgroup takes (its split), not the whole batch
+  d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), d.Bs, &bytes);
+  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
+  float* part = Sp > 1 ? ws : grads;
   const dim3 grid((unsigned)M, (unsigned)Sp);
   if (fast)
-    grad_cnn_kernel<16, 5><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out, d);
+    grad_cnn_kernel<16, 5><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part, d);
   else
-    grad_cnn_kernel<0, 0><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out, d);
+    grad_cnn_kernel<0, 0><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part, d);
   if (int rc = check_launch("grad_cnn_kernel")) return rc;
-  if (Sp > 1) {
-    reduce_splits_kernel<<<dim3((unsigned)std::min<long long>((d.P + kBlock - 1) / kBlock, 64), (unsigned)M), kBlock,
-                           0, st>>>(ws, grads, Sp, d.P);
-    return check_launch("reduce_splits_kernel");
-  }
-  return CFA_OK;
+  return Sp > 1 ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
 }
 
 int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L, int hidden, int classes,
@@ -616,26 +674,24 @@ int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L
   if (M == 0) return CFA_OK;
   if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   NnDims d;
+  if (classes > 64) return fail(CFA_E_UNSUPPORTED, "%s: more than 64 classes", fn);
   d.B = B, d.L = L, d.H = hidden, d.C = classes;
+  d.SW = softmax_width(classes);
   d.G = (L + kSpan - 1) / kSpan;
   d.P = (long long)L * hidden + hidden + (long long)hidden * classes + classes;
   long long bytes = 0;
-  d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), B, &bytes);
-  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
   int Sp = batch_split(M, B, d.P);
-  if (!ws || ws_elems < (size_t)M * Sp * (size_t)d.P) Sp = 1;
+  if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) Sp = 1;
   d.Bs = (B + Sp - 1) / Sp;
-  float* out = Sp > 1 ? ws : grads;
-  grad_2nn_kernel<<<dim3((unsigned)M, (unsigned)Sp), kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, out,
+  // LDS for the samples one workgroup takes (its split), not the whole batch
+  d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), d.Bs, &bytes);
+  if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
+  float* part = Sp > 1 ? ws : grads;
+  grad_2nn_kernel<<<dim3((unsigned)M, (unsigned)Sp), kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part,
                                                                                        d);
   if (int rc = check_launch("grad_2nn_kernel")) return rc;
-  if (Sp > 1) {
-    reduce_splits_kernel<<<dim3((unsigned)std::min<long long>((d.P + kBlock - 1) / kBlock, 64), (unsigned)M), kBlock,
-                           0, st>>>(ws, grads, Sp, d.P);
-    return check_launch("reduce_splits_kernel");
-  }
-  return CFA_OK;
+  return Sp > 1 ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
 }
 
 }  // namespace
@@ -656,7 +712,7 @@ extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L,
 
 extern "C" size_t cfa_ge_grad_workspace_elems(int M, int B, size_t P) {
   const int sp = batch_split(M, B, (long long)P);
-  return sp > 1 ? (size_t)M * sp * P : 0;
+  return sp > 1 ? split_workspace_elems(M, sp, (long long)P) : 0;
 }
 
 extern "C" int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,

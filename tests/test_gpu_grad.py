@@ -118,3 +118,36 @@ def test_rows_form_with_and_without_batch_split(gpu, ml, B, M):
             ref, _ = ref_fn(x[drow[m]], y[drow[m]], models[mrow[m]])
             for k in range(4):
                 assert normwise_close(out[m, offs[k]:offs[k + 1]], ref[k].reshape(-1), 1e-5), (m, k)
+
+
+@pytest.mark.parametrize("ml", [1, 2])
+def test_split_launch_reuses_its_workspace(gpu, ml):
+    """Back-to-back split launches on one workspace give the same bits every time, and agree with
+    the unsplit launch within the tolerance."""
+    import torch
+    rng = np.random.default_rng(50 + ml)
+    D, B, M = 16, 24, 32
+    if ml == 1:
+        geom, P = {"filter": 16, "number": 8, "stride": 5}, 16 * 8 + 8 + 21 * 8 * 8 + 8
+    else:
+        geom, P = {"intermediate_nodes": 32}, 512 * 32 + 32 + 32 * 8 + 8
+    x = torch.from_numpy(rng.standard_normal((D, B, 512)).astype(np.float32)).cuda()
+    y = torch.from_numpy(np.eye(8, dtype=np.float32)[rng.integers(0, 8, (D, B))]).cuda()
+    models = torch.from_numpy((rng.standard_normal((D, P)) * 0.1).astype(np.float32)).cuda()
+    mrow = torch.from_numpy(rng.integers(0, D, M).astype(np.int32)).cuda()
+    drow = torch.from_numpy(np.repeat(np.arange(D), 2).astype(np.int32)).cuda()
+    ws = gpu.grad_workspace(M, B, P)
+    assert ws.numel() >= 2 * M * P  # config 3 shapes do split
+    outs = []
+    for _ in range(4):
+        g = torch.full((M, P), float("nan"), device="cuda")
+        gpu.grad_rows(ml, x, y, models, mrow, drow, g, geom, workspace=ws)
+        outs.append(g)
+    torch.cuda.synchronize()
+    for g in outs[1:]:
+        assert torch.equal(g, outs[0])
+    single = torch.empty(M, P, device="cuda")
+    gpu.grad_rows(ml, x, y, models, mrow, drow, single, geom)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert float((outs[0] - single).abs().max()) <= 1e-5 * float(single.abs().max())
