@@ -81,6 +81,7 @@ SIGNATURES = {
                                      _c_void_p, _c_void_p, _c_int, _c_void_p]),
     "cfa_ge_grad_2nn_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p, _c_void_p,
                                      _c_int, _c_void_p]),
+    "cfa_ge_grad_splits": (_c_int, [_c_int, _c_int, _c_size_t]),
     "cfa_ge_grad_workspace_elems": (_c_size_t, [_c_int, _c_int, _c_size_t]),
     "cfa_ge_grad_cnn_rows_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                                           _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_size_t,
@@ -90,7 +91,8 @@ SIGNATURES = {
                                           _c_void_p]),
     "cfa_ge_population_step_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                             _c_void_p, _c_int, ctypes.c_double, ctypes.c_float, ctypes.c_float,
-                                            _c_size_t, _c_int, _c_size_t, _c_void_p]),
+                                            _c_size_t, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_int, _c_int,
+                                            _c_void_p]),
     "cfa_comm_unique_id": (_c_int, [_c_void_p]),
     "cfa_comm_init": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_void_p, _c_int]),
     "cfa_comm_destroy": (_c_int, [_c_void_p]),

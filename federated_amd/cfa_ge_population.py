@@ -14,8 +14,9 @@ in HBM and one round of the fast negotiation is four steps on the GPU:
 4. (:491-535) every device evaluates the gradient of its own cost at each neighbour's
    previous-round model.
 
-Steps 1 and 3 are ONE ``cfa_ge_population_step_f32`` launch for all devices, step 4 ONE
-``cfa_ge_grad_{cnn,2nn}_rows_f32`` launch for all D*N (device, neighbour) pairs.
+Step 4 is ONE ``cfa_ge_grad_{cnn,2nn}_rows_f32`` launch for all D*N (device, neighbour) pairs,
+leaving partial sums per batch split; steps 1 and 3 for all devices and the sum of those
+partials are ONE ``cfa_ge_population_step_f32`` launch. A round is two launches.
 
 Buckets are fp32 (the population is device-resident; the drop-in modules keep the reference's
 fp64 host arithmetic). A round equals ``oracle.cfa_ge_population_round`` within 1e-5 normwise.
@@ -89,7 +90,10 @@ class CfaGePopulation:
         # gradient evaluations: pair (i, n) -> model row lists[i][n] of pub, data row i
         mrow = [j for i, nb in enumerate(self.lists) for j in nb + [0] * (Nmax - len(nb))]
         drow = [i for i, nb in enumerate(self.lists) for _ in range(Nmax)]
-        self._ws = engine.grad_workspace(len(mrow), int(x.shape[1]), P)  # batch split over workgroups
+        # the gradient launch leaves [M][splits][P] partial sums (each evaluation's batch split over
+        # workgroups); the next population-step launch sums them into G_next
+        self._splits = engine.grad_splits(len(mrow), int(x.shape[1]), P)
+        self._ws = torch.empty(len(mrow) * self._splits * P, device=dev)
         self._mrow = torch.tensor(mrow, dtype=torch.int32, device=dev)
         self._drow = torch.tensor(drow, dtype=torch.int32, device=dev)
         # where device i finds slot i of neighbour j's gradients: G row j*N + m (last m with
@@ -151,12 +155,15 @@ class CfaGePopulation:
         eng, D, P = self.engine, self.D, self.P
         ptr, idx, coef = self._csr
         src, dst = self._tables[self._rot]
-        # 4: gradients of every device's cost at its neighbours' previous-round models
-        eng.grad_rows(self.ml_model, self.x, self.y, self.pub, self._mrow, self._drow, self.G_next,
+        # 4: gradients of every device's cost at its neighbours' previous-round models (partial
+        # sums per batch split)
+        eng.grad_rows(self.ml_model, self.x, self.y, self.pub, self._mrow, self._drow, None,
                       self.geom, stream, workspace=self._ws)
-        # 1 + 3: stage-1 mix and the gradient step with the previous round's gradients, one launch
+        # 1 + 3: stage-1 mix and the gradient step with the previous round's gradients, and the
+        # sum of this round's partial gradients into G_next, one launch
         eng.ge_population_step(dst, src, self._states, self._grads[self._gpar], ptr, idx, coef, D, self.rho,
-                               self.lr1, self.lr2, self.lr_split, self.ml_model == 1, P, stream)
+                               self.lr1, self.lr2, self.lr_split, self.ml_model == 1, P, stream,
+                               reduce=(self._ws, self.G_next, self._splits))
         # 2: the pre-mix local models are this round's published models; the new locals are the
         # updated mixes; this round's gradients become the next round's input
         self._rot = (self._rot + 2) % 3  # (W, pub, mixed) <- (mixed, W, pub)

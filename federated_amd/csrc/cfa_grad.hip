@@ -634,7 +634,7 @@ int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L
     return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d C %d F %d NC %d S %d M %d)", fn, B, L, classes,
                 filter, number, stride, M);
   if (M == 0) return CFA_OK;
-  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
+  if (!x || !y || !models || (!grads && !ws)) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   CnnDims d;
   if (classes > 64) return fail(CFA_E_UNSUPPORTED, "%s: more than 64 classes", fn);
   d.B = B, d.L = L, d.C = classes, d.F = filter, d.NC = number, d.S = stride;
@@ -651,19 +651,25 @@ int launch_grad_cnn(const char* fn, const float* x, const float* y, int B, int L
   const void* kern = fast ? (const void*)grad_cnn_kernel<16, 5> : (const void*)grad_cnn_kernel<0, 0>;
   hipStream_t st = static_cast<hipStream_t>(stream);
   int Sp = batch_split(M, B, d.P);
-  if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) Sp = 1;
+  if (!grads) {  // partials only: [M][Sp][P] into the workspace, summed by the caller
+    if (ws_elems < split_workspace_elems(M, Sp, d.P))
+      return fail(CFA_E_INVALID, "%s: partials-only launch needs %zu workspace floats", fn,
+                  split_workspace_elems(M, Sp, d.P));
+  } else if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) {
+    Sp = 1;
+  }
   d.Bs = (B + Sp - 1) / Sp;
   // LDS for the samples one workgroup takes (its split), not the whole batch
   d.Bc = plan_chunk(kern, cnn_lds_fixed(d), cnn_lds_per_sample(d), d.Bs, &bytes);
   if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
-  float* part = Sp > 1 ? ws : grads;
+  float* part = (Sp > 1 || !grads) ? ws : grads;
   const dim3 grid((unsigned)M, (unsigned)Sp);
   if (fast)
     grad_cnn_kernel<16, 5><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part, d);
   else
     grad_cnn_kernel<0, 0><<<grid, kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part, d);
   if (int rc = check_launch("grad_cnn_kernel")) return rc;
-  return Sp > 1 ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
+  return (Sp > 1 && grads) ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
 }
 
 int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L, int hidden, int classes,
@@ -672,7 +678,7 @@ int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L
   if (M < 0 || B < 1 || L < 1 || hidden < 1 || classes < 1)
     return fail(CFA_E_INVALID, "%s: bad dimensions (B %d L %d H %d C %d M %d)", fn, B, L, hidden, classes, M);
   if (M == 0) return CFA_OK;
-  if (!x || !y || !models || !grads) return fail(CFA_E_INVALID, "%s: null buffer", fn);
+  if (!x || !y || !models || (!grads && !ws)) return fail(CFA_E_INVALID, "%s: null buffer", fn);
   NnDims d;
   if (classes > 64) return fail(CFA_E_UNSUPPORTED, "%s: more than 64 classes", fn);
   d.B = B, d.L = L, d.H = hidden, d.C = classes;
@@ -682,16 +688,22 @@ int launch_grad_2nn(const char* fn, const float* x, const float* y, int B, int L
   long long bytes = 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   int Sp = batch_split(M, B, d.P);
-  if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) Sp = 1;
+  if (!grads) {  // partials only: [M][Sp][P] into the workspace, summed by the caller
+    if (ws_elems < split_workspace_elems(M, Sp, d.P))
+      return fail(CFA_E_INVALID, "%s: partials-only launch needs %zu workspace floats", fn,
+                  split_workspace_elems(M, Sp, d.P));
+  } else if (!ws || ws_elems < split_workspace_elems(M, Sp, d.P)) {
+    Sp = 1;
+  }
   d.Bs = (B + Sp - 1) / Sp;
   // LDS for the samples one workgroup takes (its split), not the whole batch
   d.Bc = plan_chunk((const void*)grad_2nn_kernel, nn_lds_fixed(d), nn_lds_per_sample(d), d.Bs, &bytes);
   if (d.Bc < 1) return fail(CFA_E_UNSUPPORTED, "%s: one sample does not fit the workgroup's LDS", fn);
-  float* part = Sp > 1 ? ws : grads;
+  float* part = (Sp > 1 || !grads) ? ws : grads;
   grad_2nn_kernel<<<dim3((unsigned)M, (unsigned)Sp), kGradBlock, (size_t)bytes, st>>>(x, y, models, mrow, drow, part,
                                                                                        d);
   if (int rc = check_launch("grad_2nn_kernel")) return rc;
-  return Sp > 1 ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
+  return (Sp > 1 && grads) ? launch_reduce_splits(ws, grads, M, Sp, d.P, st) : CFA_OK;
 }
 
 }  // namespace
@@ -709,6 +721,8 @@ extern "C" int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L,
   return launch_grad_2nn("cfa_ge_grad_2nn_f32", x, y, B, L, hidden, classes, models, nullptr, nullptr, grads,
                          nullptr, 0, M, stream);
 }
+
+extern "C" int cfa_ge_grad_splits(int M, int B, size_t P) { return batch_split(M, B, (long long)P); }
 
 extern "C" size_t cfa_ge_grad_workspace_elems(int M, int B, size_t P) {
   const int sp = batch_split(M, B, (long long)P);

@@ -326,12 +326,27 @@ struct GeStepArgs {
   float rho, one_minus_rho, lr1, lr2;
   long long split;
   int filtered;
+  // optional second job of the same launch: sum rsp partial buckets of rM gradient evaluations
+  // (rws [rM][rsp][P], written by a partials-only cfa_ge_grad_*_rows_f32) into rout [rM][P]
+  const float* rws;
+  float* rout;
+  int rM, rsp;
 };
 
 __device__ __forceinline__ float ge_lr(const GeStepArgs& a, long long i) { return i < a.split ? a.lr1 : a.lr2; }
 
 __global__ __launch_bounds__(kBlock) void ge_step_kernel(GeStepArgs a, long long nvec, long long P) {
   const int d = blockIdx.y;
+  if (d >= (int)gridDim.y - a.rM) {  // reduction rows: the split sum in split order (deterministic)
+    const long long m = d - ((int)gridDim.y - a.rM);
+    const float* w = a.rws + m * a.rsp * P;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += (long long)gridDim.x * kBlock) {
+      float s = w[i];
+      for (int sp = 1; sp < a.rsp; ++sp) s += w[(long long)sp * P + i];
+      a.rout[m * P + i] = s;
+    }
+    return;
+  }
   const int e0 = a.ptr[d], e1 = a.ptr[d + 1];
   float* out = a.out[d];
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
@@ -384,21 +399,26 @@ extern "C" int cfa_ge_population_step_f32(float* const* out_ptrs, const float* c
                                           const int32_t* csr_ptr, const int32_t* csr_idx,
                                           const float* csr_coef, int D, double rho, float lr1,
                                           float lr2, size_t lr_split, int use_filtered, size_t P,
-                                          void* stream) {
+                                          const float* reduce_ws, float* reduce_out, int reduce_M,
+                                          int reduce_splits, void* stream) {
   if (D < 0) return fail(CFA_E_INVALID, "negative device count");
-  if (D == 0 || P == 0) return CFA_OK;
-  if (!out_ptrs || !src_ptrs || !state_ptrs || !grad_ptrs || !csr_ptr || !csr_idx || !csr_coef)
+  if (!reduce_ws) reduce_M = 0;
+  if (reduce_M < 0 || (reduce_M > 0 && (!reduce_out || reduce_splits < 1)))
+    return fail(CFA_E_INVALID, "bad split reduction (M %d, splits %d)", reduce_M, reduce_splits);
+  if ((D == 0 && reduce_M == 0) || P == 0) return CFA_OK;
+  if (D > 0 && (!out_ptrs || !src_ptrs || !state_ptrs || !grad_ptrs || !csr_ptr || !csr_idx || !csr_coef))
     return fail(CFA_E_INVALID, "null population table");
-  if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
+  if ((long long)D + reduce_M > 65535) return fail(CFA_E_INVALID, "D + M = %d exceeds grid.y limit", D + reduce_M);
   GeStepArgs a{out_ptrs, src_ptrs, state_ptrs, grad_ptrs, csr_ptr, csr_idx, csr_coef,
-               (float)rho, (float)(1.0 - rho), lr1, lr2, (long long)lr_split, use_filtered ? 1 : 0};
+               (float)rho, (float)(1.0 - rho), lr1, lr2, (long long)lr_split, use_filtered ? 1 : 0,
+               reduce_ws, reduce_out, reduce_M, reduce_splits};
   // buckets are 16-byte aligned (allocator contract, checked by the host layer)
   const long long nvec = (long long)P / 4;
   long long gx = (nvec + kBlock - 1) / kBlock;
-  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  const long long cap = ((long long)device_cus() * 8 + D + reduce_M - 1) / (D + reduce_M);
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
-  dim3 grid((unsigned)gx, (unsigned)D);
+  dim3 grid((unsigned)gx, (unsigned)(D + reduce_M));
   ge_step_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(a, nvec, (long long)P);
   return check_launch("ge_step_kernel");
 }

@@ -350,18 +350,32 @@ class Engine:
         n = int(_lib.load().cfa_ge_grad_workspace_elems(int(M), int(B), int(P)))
         return torch.empty(max(n, 1), dtype=torch.float32, device=self.device)
 
+    def grad_splits(self, M: int, B: int, P: int) -> int:
+        """Workgroups per evaluation of a split gradient launch (cfa_ge_grad_splits)."""
+        return int(_lib.load().cfa_ge_grad_splits(int(M), int(B), int(P)))
+
     def grad_rows(self, ml_model: int, x: torch.Tensor, y: torch.Tensor, models: torch.Tensor,
-                  model_row: torch.Tensor, data_row: torch.Tensor, grads: torch.Tensor, geom: dict,
-                  stream=None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  model_row: torch.Tensor, data_row: torch.Tensor, grads: Optional[torch.Tensor], geom: dict,
+                  stream=None, workspace: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         """Population form (cfa_ge_grad_{cnn,2nn}_rows_f32): evaluation m = gradient of data row
         data_row[m] (x [Dx, B, L], y [Dx, B, C]) at model row model_row[m] of models [Dm, P],
         into grads [M, P]. ``geom``: filter/number/stride (CNN) or intermediate_nodes (2NN).
-        ``workspace`` (``grad_workspace``) lets each evaluation's batch spread over workgroups."""
+        ``workspace`` (``grad_workspace``) lets each evaluation's batch spread over workgroups.
+        ``grads=None``: partials only, [M][grad_splits(M, B, P)][P] into ``workspace`` (at least
+        that size), summed later by ``ge_population_step(..., reduce=...)``."""
         for name, t, nd in (("x", x, 3), ("y", y, 3)):
             if not t.is_cuda or t.dtype != torch.float32 or t.dim() != nd or not t.is_contiguous():
                 raise TypeError(f"{name} must be a contiguous 3-D fp32 CUDA tensor")
         Dm, P = _check_2d(models, "models")
-        M, Pg = _check_2d(grads, "grads")
+        if grads is None:
+            if workspace is None:
+                raise ValueError("a partials-only launch (grads=None) needs a workspace")
+            M, Pg = int(model_row.numel()), P
+            need = M * self.grad_splits(M, int(x.shape[1]), P) * P
+            if workspace.numel() < need:
+                raise ValueError(f"partials-only launch needs a workspace of {need} floats")
+        else:
+            M, Pg = _check_2d(grads, "grads")
         for name, t in (("model_row", model_row), ("data_row", data_row)):
             if not t.is_cuda or t.dtype != torch.int32 or t.numel() != M or not t.is_contiguous():
                 raise TypeError(f"{name} must be a contiguous int32 CUDA tensor of {M} entries")
@@ -380,15 +394,15 @@ class Engine:
             if P != F * NC + NC + L2 * NC * C + C:
                 raise ValueError("CNN bucket size does not match the geometry")
             _lib.call("cfa_ge_grad_cnn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, C, F, NC, S, models.data_ptr(),
-                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), ws_ptr, ws_n, M,
-                      self.stream_handle(stream))
+                      model_row.data_ptr(), data_row.data_ptr(), None if grads is None else grads.data_ptr(), ws_ptr,
+                      ws_n, M, self.stream_handle(stream))
         elif ml_model == 2:
             H = int(geom["intermediate_nodes"])
             if P != L * H + H + H * C + C:
                 raise ValueError("2NN bucket size does not match the geometry")
             _lib.call("cfa_ge_grad_2nn_rows_f32", x.data_ptr(), y.data_ptr(), B, L, H, C, models.data_ptr(),
-                      model_row.data_ptr(), data_row.data_ptr(), grads.data_ptr(), ws_ptr, ws_n, M,
-                      self.stream_handle(stream))
+                      model_row.data_ptr(), data_row.data_ptr(), None if grads is None else grads.data_ptr(), ws_ptr,
+                      ws_n, M, self.stream_handle(stream))
         else:
             raise ValueError("ml_model must be 1 (CNN) or 2 (2NN)")
         return grads
@@ -419,9 +433,11 @@ class Engine:
     def ge_population_step(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, state_ptrs: torch.Tensor,
                            grad_ptrs: torch.Tensor, csr_ptr: torch.Tensor, csr_idx: torch.Tensor,
                            csr_coef: torch.Tensor, D: int, rho: float, lr1: float, lr2: float, lr_split: int,
-                           use_filtered: bool, P: int, stream=None) -> None:
+                           use_filtered: bool, P: int, stream=None, reduce=None) -> None:
         """cfa_ge_population_step_f32: stage-1 mix + MEWMA gradient step of D devices in one
-        launch; pointer tables are int64 CUDA tensors aligned with the CSR entries."""
+        launch; pointer tables are int64 CUDA tensors aligned with the CSR entries.
+        ``reduce=(workspace, out [M, P], splits)``: the same launch also sums a partials-only
+        gradient launch's [M][splits][P] workspace into ``out``."""
         for name, t, dt in (("out_ptrs", out_ptrs, torch.int64), ("src_ptrs", src_ptrs, torch.int64),
                             ("state_ptrs", state_ptrs, torch.int64), ("grad_ptrs", grad_ptrs, torch.int64),
                             ("csr_ptr", csr_ptr, torch.int32), ("csr_idx", csr_idx, torch.int32),
@@ -431,10 +447,19 @@ class Engine:
         E = csr_idx.numel()
         if csr_ptr.numel() != D + 1 or out_ptrs.numel() != D or state_ptrs.numel() != E or grad_ptrs.numel() != E:
             raise ValueError("tables: D+1 row pointers, D outputs, one state and one gradient slot per CSR entry")
+        r_ws = r_out = None
+        r_M = r_sp = 0
+        if reduce is not None:
+            ws, out, r_sp = reduce
+            r_M, Po = _check_2d(out, "reduce out")
+            r_sp = int(r_sp)
+            if Po != P or r_sp < 1 or not ws.is_cuda or ws.dtype != torch.float32 or ws.numel() < r_M * r_sp * P:
+                raise ValueError("reduce: out [M, P] and a workspace of M * splits * P fp32 elements")
+            r_ws, r_out = ws.data_ptr(), out.data_ptr()
         _lib.call("cfa_ge_population_step_f32", out_ptrs.data_ptr(), src_ptrs.data_ptr(), state_ptrs.data_ptr(),
                   grad_ptrs.data_ptr(), csr_ptr.data_ptr(), csr_idx.data_ptr(), csr_coef.data_ptr(), int(D),
-                  float(rho), float(lr1), float(lr2), int(lr_split), int(bool(use_filtered)), int(P),
-                  self.stream_handle(stream))
+                  float(rho), float(lr1), float(lr2), int(lr_split), int(bool(use_filtered)), int(P), r_ws, r_out,
+                  int(r_M), int(r_sp), self.stream_handle(stream))
 
     def population(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
                    csr_idx: torch.Tensor, csr_coef: torch.Tensor, D: int, rule: int, P: int,

@@ -261,7 +261,11 @@ CFA_API int cfa_ge_grad_2nn_f32(const float* x, const float* y, int B, int L, in
  * gradient of device data_row[m]'s cost at device model_row[m]'s published model. With a device
  * `workspace` of at least cfa_ge_grad_workspace_elems(M, B, P) floats, each evaluation's batch is
  * split over several workgroups (about two per CU in all) whose partial sums are then added in a
- * fixed order (deterministic); with less (or NULL) one workgroup takes each evaluation. */
+ * fixed order (deterministic); with less (or NULL) one workgroup takes each evaluation.
+ * grads == NULL: partials only. The launch writes [M][S][P] partial buckets to `workspace`
+ * (S = cfa_ge_grad_splits(M, B, P); at least M * S * P floats) and the caller sums them, e.g. in
+ * the same launch as the next population step (cfa_ge_population_step_f32's reduce_* args). */
+CFA_API int cfa_ge_grad_splits(int M, int B, size_t P);
 CFA_API size_t cfa_ge_grad_workspace_elems(int M, int B, size_t P);
 CFA_API int cfa_ge_grad_cnn_rows_f32(const float* x, const float* y, int B, int L, int classes,
                                      int filter, int number, int stride, const float* models,
@@ -291,12 +295,20 @@ CFA_API int cfa_mix_population_f32(float* const* out_ptrs, const float* const* s
  *   s <- rho * g + (1 - rho) * s   (s = state_ptrs[e], g = grad_ptrs[e], NULL = zero gradient)
  *   w <- w - lr(i) * (use_filtered ? s : g),   lr(i) = i < lr_split ? lr1 : lr2
  * and out_ptrs[d] = w. Every table is a DEVICE array; entry e0's state/grad slots are unused.
- * Same operations, same order, same results as cfa_mix_population_f32 + cfa_mewma_update_f32. */
+ * Same operations, same order, same results as cfa_mix_population_f32 + cfa_mewma_update_f32.
+ * reduce_ws != NULL: the same launch also sums the reduce_splits partial buckets of reduce_M
+ * gradient evaluations (reduce_ws [reduce_M][reduce_splits][P], from a partials-only
+ * cfa_ge_grad_*_rows_f32) into reduce_out [reduce_M][P], in split order: the same sums as the
+ * rows launch's own reduction. A CFA-GE round is then two launches: the gradients of this round
+ * (partials), and this step (previous round's gradients) + this round's reduction.
+ * reduce_out must not alias any table or bucket the step reads. */
 CFA_API int cfa_ge_population_step_f32(float* const* out_ptrs, const float* const* src_ptrs,
                                        float* const* state_ptrs, const float* const* grad_ptrs,
                                        const int32_t* csr_ptr, const int32_t* csr_idx,
                                        const float* csr_coef, int D, double rho, float lr1, float lr2,
-                                       size_t lr_split, int use_filtered, size_t P, void* stream);
+                                       size_t lr_split, int use_filtered, size_t P,
+                                       const float* reduce_ws, float* reduce_out, int reduce_M,
+                                       int reduce_splits, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Multi-GPU (RCCL over xGMI): one process per GPU.

@@ -93,3 +93,47 @@ def test_fused_step_equals_mix_then_mewma(gpu, P, filtered):
         assert torch.equal(out1[i], out2[i]), i
         for n in range(len(lists[i])):
             assert torch.equal(S[i][n], S2[i][n]), (i, n)
+
+
+@pytest.mark.parametrize("ml", [1, 2])
+def test_partials_reduced_in_step_launch_equal_rows_reduction(gpu, ml):
+    """A partials-only gradient launch summed by cfa_ge_population_step_f32's reduction rows
+    equals the rows launch's own reduction bit for bit, and the step's outputs are unchanged by
+    the extra rows."""
+    from federated_amd import topology
+    rng = np.random.default_rng(77 + ml)
+    D, N, B = 16, 2, 24
+    geom = {"filter": 16, "number": 8, "stride": 5} if ml == 1 else {"intermediate_nodes": 32}
+    full = {**geom, "input_data": 512, "classes": 8}
+    P = sum(int(np.prod(s)) for s in orc.tf1_flat_shapes(ml, full))
+    lists = topology.kregular_tf1(D, N)
+    x = torch.from_numpy(rng.standard_normal((D, B, 512)).astype(np.float32)).cuda()
+    y = torch.from_numpy(np.eye(8, dtype=np.float32)[rng.integers(0, 8, (D, B))]).cuda()
+    models = torch.from_numpy((rng.standard_normal((D, P)) * 0.1).astype(np.float32)).cuda()
+    mrow = torch.tensor([j for nb in lists for j in nb], dtype=torch.int32, device="cuda")
+    drow = torch.tensor([i for i, nb in enumerate(lists) for _ in nb], dtype=torch.int32, device="cuda")
+    M = mrow.numel()
+    Sp = gpu.grad_splits(M, B, P)
+    assert Sp > 1
+    ref = torch.empty(M, P, device="cuda")
+    gpu.grad_rows(ml, x, y, models, mrow, drow, ref, geom, workspace=gpu.grad_workspace(M, B, P))
+    ws = torch.empty(M * Sp * P, device="cuda")
+    gpu.grad_rows(ml, x, y, models, mrow, drow, None, geom, workspace=ws)
+    # a small population step alongside the reduction
+    t = lambda v, dt: torch.tensor(v, dtype=dt, device="cuda")
+    W = torch.randn(2, P, device="cuda")
+    S1, S2 = torch.randn(P, device="cuda"), None
+    S2 = S1.clone()
+    g = torch.randn(P, device="cuda")
+    outs = [torch.empty(P, device="cuda") for _ in range(2)]
+    src = t([W[0].data_ptr(), W[1].data_ptr()], torch.int64)
+    tabs = (t([0, 2], torch.int32), t([0, 1], torch.int32), t([0.0, 0.4], torch.float32))
+    got = torch.full((M, P), float("nan"), device="cuda")
+    gpu.ge_population_step(t([outs[0].data_ptr()], torch.int64), src, t([0, S1.data_ptr()], torch.int64),
+                           t([0, g.data_ptr()], torch.int64), *tabs, 1, 0.99, 0.1, 0.05, 5, True, P,
+                           reduce=(ws, got, Sp))
+    gpu.ge_population_step(t([outs[1].data_ptr()], torch.int64), src, t([0, S2.data_ptr()], torch.int64),
+                           t([0, g.data_ptr()], torch.int64), *tabs, 1, 0.99, 0.1, 0.05, 5, True, P)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(S1, S2)
