@@ -12,6 +12,7 @@ the eager rounds' results bit for bit (tested in tests/test_gpu_graph_rounds.py)
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, Dict, Tuple
 
 import torch
@@ -39,10 +40,19 @@ class RoundGraphs:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            # "relaxed": the libcfa launch path may query device attributes during capture
-            with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
-                for _ in range(periods * self.period):
-                    self.step()
+            # no garbage collection while capturing: collecting an unrelated dead graph, event or
+            # stream would destroy a HIP object mid-capture and abort the process
+            gc.collect()
+            was_enabled = gc.isenabled()
+            gc.disable()
+            try:
+                # "relaxed": the libcfa launch path may query device attributes during capture
+                with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+                    for _ in range(periods * self.period):
+                        self.step()
+            finally:
+                if was_enabled:
+                    gc.enable()
             if self.phase() != key[0]:
                 raise RuntimeError("a period of rounds must return to its starting phase")
             self._graphs[key] = g

@@ -53,14 +53,16 @@ def test_population_rounds_match_oracle(gpu, ml, D, N):
         rW, rpub, rS, rG = gW.astype(np.float64), gpub.astype(np.float64), gS.astype(np.float64), gG.astype(np.float64)
 
 
-@pytest.mark.parametrize("P,filtered", [(1488, True), (1001, False), (7, True)])
-def test_fused_step_equals_mix_then_mewma(gpu, P, filtered):
+@pytest.mark.parametrize("P,filtered,wide", [(1488, True, False), (1001, False, False), (7, True, False),
+                                             (1488, True, True), (1001, False, True)])
+def test_fused_step_equals_mix_then_mewma(gpu, P, filtered, wide):
     """cfa_ge_population_step_f32 == cfa_mix_population_f32 followed by cfa_mewma_update_f32,
     bit for bit (separate 16-byte-aligned allocations so P % 4 != 0 exercises the tail; one
     neighbour slot without gradients)."""
     from federated_amd import _lib
     D = 4
-    lists = [[1, 2], [0], [3, 0, 1], []]
+    # wide: a device with 7 neighbours takes the kernel's looped path (more entries than registers)
+    lists = [[1, 2, 3, 0, 2, 3, 1] if wide else [1, 2], [0], [3, 0, 1], []]
     g = torch.Generator(device="cuda").manual_seed(P)
     rnd = lambda: torch.randn(P, device="cuda", generator=g)
     W = [rnd() for _ in range(D)]
