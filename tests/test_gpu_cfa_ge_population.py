@@ -61,7 +61,7 @@ def test_fused_step_equals_mix_then_mewma(gpu, P, filtered, wide):
     neighbour slot without gradients)."""
     from federated_amd import _lib
     D = 4
-    # wide: a device with 7 neighbours takes the kernel's looped path (more entries than registers)
+    # wide: a device with 7 neighbours (longer fold and gradient chains)
     lists = [[1, 2, 3, 0, 2, 3, 1] if wide else [1, 2], [0], [3, 0, 1], []]
     g = torch.Generator(device="cuda").manual_seed(P)
     rnd = lambda: torch.randn(P, device="cuda", generator=g)
