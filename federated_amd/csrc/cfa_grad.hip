@@ -25,16 +25,27 @@ constexpr float kClipLo = 1e-15f, kClipHi = 0.99f;
 
 // Phase timestamps for tools/probe/grad_phases.hip (compiled out of the library).
 #ifdef CFA_GRAD_PHASES
+// Stamps go to LDS and are copied out at the last phase (8 / 17), so no phase waits on the
+// previous stamp's global store.
 __device__ unsigned long long g_phase[32];
 __device__ unsigned long long g_wg[4096][2];  // per workgroup: first and last stamp
+__device__ __forceinline__ unsigned long long* phase_lds() {
+  __shared__ unsigned long long s[32];  // one array per kernel, shared by every PHASE site
+  return s;
+}
 #define PHASE(k) \
   do {           \
+    unsigned long long* s_ts_ = phase_lds(); \
     __syncthreads(); \
     if (threadIdx.x == 0) { \
-      const unsigned long long t_ = wall_clock64(); \
-      const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x; \
-      if (blockIdx.x == 0 && blockIdx.y == 0) g_phase[k] = t_; \
-      if (wg_ < 4096) g_wg[wg_][(k) == 0 || (k) == 10 ? 0 : 1] = t_; \
+      s_ts_[k] = wall_clock64(); \
+      if ((k) == 8 || (k) == 17) { \
+        const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x; \
+        const int k0_ = (k) == 8 ? 0 : 10; \
+        if (blockIdx.x == 0 && blockIdx.y == 0) \
+          for (int j_ = k0_; j_ <= (k); ++j_) g_phase[j_] = s_ts_[j_]; \
+        if (wg_ < 4096) g_wg[wg_][0] = s_ts_[k0_], g_wg[wg_][1] = s_ts_[k]; \
+      } \
     } \
   } while (0)
 #else
@@ -198,8 +209,19 @@ __global__ __launch_bounds__(kGradBlock) void grad_cnn_kernel(const float* __res
   // item a thread takes below has the same channel c = tid % NC)
   const bool taps_in_regs = d.F <= kMaxTaps && T % d.NC == 0;
   float wreg[kMaxTaps];
+  {
+    // one channel index and one uniform branch around every tap load (a per-tap predicate
+    // recomputed the modulo and branched 32 times: 2.6 us at the config-3 shapes)
+    const int creg = tid % d.NC;
+    constexpr int KT = FT > 0 ? FT : kMaxTaps;
 #pragma unroll
-  for (int k = 0; k < kMaxTaps; ++k) wreg[k] = (taps_in_regs && k < d.F) ? W1[k * d.NC + tid % d.NC] : 0.f;
+    for (int k = 0; k < kMaxTaps; ++k) wreg[k] = 0.f;
+    if (taps_in_regs) {
+#pragma unroll
+      for (int k = 0; k < KT; ++k)
+        if (FT > 0 || k < d.F) wreg[k] = W1[k * d.NC + creg];
+    }
+  }
   if (bb >= be) {  // no sample left for this split: a zero partial
     for (long long i = threadIdx.x; i < d.P; i += blockDim.x) g[i] = 0.f;
     return;
