@@ -179,7 +179,10 @@ static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long l
 template <int RULE>
 static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
                              const cfa_launch_t& t) {
-  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : auto_vec(n);
+  // the divisor fold carries a guarded division per element and step: one float4 per lane
+  // keeps more tiles in flight per VGPR budget (tools/probe/div_sweep.py: 6.03 vs 5.69 TB/s)
+  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane)
+                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : auto_vec(n));
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   const unsigned grid = grid_for(tiles, t);
   if (U == 4) {
@@ -239,6 +242,7 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
     for (int j = 0; j < n; ++j) f.src[j + 1] = nbrs[j] + head;
     for (int k = 0; k <= n; ++k) f.c[k] = c[k];
     for (int k = 0; k <= n; ++k) f.d[k] = div ? div[k] : 1.0f;
+    set_reciprocals(f, n);
     if (cp) {
       CompressParams shifted = cpv;
       shifted.cbegin = cpv.cbegin - (long long)head;

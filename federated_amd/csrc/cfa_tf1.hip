@@ -101,8 +101,23 @@ struct F64Fanin {
   const double* src[CFA_MAX_FANIN + 1];  // [0] = running w (local or previous pass), [1..m]
   double a[CFA_MAX_FANIN + 1];
   double d[CFA_MAX_FANIN + 1];           // SEQUENTIAL_DIV divisors
+  double r[CFA_MAX_FANIN + 1];           // RN(1 / d[j]) for ddiv_rn
   int m;
+  int fast_div;                          // every d[j] in [2^-20, 2^20]
 };
+
+// fp64 counterpart of div_rn (cfa_internal.h): Markstein's correction from RN(1/b) is the
+// correctly rounded quotient when nothing under- or overflows; |a| in [2^-900, 2^900] and b in
+// [2^-20, 2^20] guarantee that, everything else takes the IEEE division.
+__device__ __forceinline__ double ddiv_rn(double a, double b, double rb, bool fast) {
+  const double aa = __builtin_fabs(a);
+  if (fast && aa >= 0x1p-900 && aa <= 0x1p900) {
+    const double q = a * rb;
+    const double r = __builtin_fma(-q, b, a);
+    return __builtin_fma(r, rb, q);
+  }
+  return a / b;
+}
 // rule: CFA_RULE_SEQUENTIAL  w = w + a*(x - w)
 //       CFA_RULE_SEQUENTIAL_DIV  w = w + (a*(x - w))/d
 //       CFA_RULE_ACCUMULATE  w = w + a*x
@@ -175,7 +190,8 @@ __global__ __launch_bounds__(kBlock) void fold_f64_vec_kernel(double* out, F64Fa
         for (int k = 1; k <= N; ++k) {
           if (k < j) continue;
           if constexpr (RULE == CFA_RULE_SEQUENTIAL) w = w + f.a[k] * (v[u][k][c] - w);
-          else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV) w = w + (f.a[k] * (v[u][k][c] - w)) / f.d[k];
+          else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV)
+            w = w + ddiv_rn(f.a[k] * (v[u][k][c] - w), f.d[k], f.r[k], f.fast_div);
           else w = w + f.a[k] * v[u][k][c];
         }
         if (compress) {
@@ -472,7 +488,11 @@ int fold_f64(double* out, const double* local, const double* const* nbrs, const 
       f.src[j + 1] = nbrs[done + j];
       f.a[j + 1] = alphas[done + j];
       f.d[j + 1] = divisors ? divisors[done + j] : 1.0;
+      f.r[j + 1] = 1.0 / f.d[j + 1];
     }
+    f.fast_div = 1;
+    for (int j = 1; j <= m; ++j)
+      if (!(f.d[j] >= 0x1p-20 && f.d[j] <= 0x1p20)) f.fast_div = 0;
     const int s0 = done == 0 ? step0_f32 : 0;
     const int cmp = last ? compress : 0;
     bool aligned = m >= 1 && (addr(out) & 15) == 0 && (addr(w) & 15) == 0 && (!cmp || (addr(local) & 15) == 0);

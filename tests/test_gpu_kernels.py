@@ -491,3 +491,63 @@ def test_special_values_follow_numpy(gpu, n):
     o64 = torch.empty(P, dtype=torch.float64, device="cuda")
     gpu.mix_tf1_f64(o64, _dev(l64), [_dev(x) for x in n64], a64, False)
     assert _same_bits_or_nan(o64.cpu().numpy(), r64)
+
+
+@pytest.mark.parametrize("divisors", [[float(c) for c in range(1, 65)],
+                                      [3.0, 7.0, 1e-7, 3e7, 0.1, 1023.0, 2.0 ** 20, 2.0 ** -20],
+                                      [float(c) for c in (97, 255, 4095, 65535, 1048575)]])
+def test_mix_seq_div_quotient_exact_over_exponent_range(gpu, divisors):
+    """The fold's division (reciprocal + one fma correction inside a range guard, IEEE division
+    outside it) equals numpy's fp32 a / C bit for bit: with local = 0 and u = 1 the one-step fold
+    is 0 + x / C, for x spread over every binade from 2^-149 to 2^127 (zeros, subnormals, the
+    guard's edges, infinities and NaN included) and divisors inside and outside the fast range."""
+    rng = np.random.default_rng(4242)
+    P = 1 << 22
+    mant = rng.integers(0, 1 << 23, P, dtype=np.uint32)
+    expo = rng.integers(0, 255, P, dtype=np.uint32)  # every biased exponent but inf/nan
+    sign = rng.integers(0, 2, P, dtype=np.uint32) << 31
+    x = (sign | (expo << 23) | mant).view(np.float32)
+    edges = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 2.0 ** -100, -(2.0 ** -100), 2.0 ** 100,
+                      np.nextafter(np.float32(2.0 ** -100), np.float32(0)), np.nextafter(np.float32(2.0 ** 100),
+                                                                                  np.float32(np.inf)),
+                      1.0, 3.0, 1e-45, 3.4028235e38], dtype=np.float32)
+    x[:edges.size] = edges
+    xd = _dev(x)
+    zero = torch.zeros(P, device="cuda")
+    out = torch.empty(P, device="cuda")
+    with np.errstate(all="ignore"):
+        for C in divisors:
+            gpu.mix_seq_div(out, zero, [xd], [1.0], [C])
+            ref = np.float32(0.0) + (np.float32(1.0) * (x - np.float32(0.0))) / np.float32(C)
+            got = out.cpu().numpy()
+            same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+            assert same.all(), (C, x[~same][:4], got[~same][:4], ref[~same][:4])
+
+
+@pytest.mark.parametrize("divisors", [[float(c) for c in range(1, 33)], [3.0, 1e-6, 7e5, 0.1, 2.0 ** 20, 2.0 ** -20]])
+def test_fold_f64_div_quotient_exact_over_exponent_range(gpu, divisors):
+    """fp64 divisor fold (cfa_fold_f64, SEQUENTIAL_DIV): with local = 0 and u = 1 the one-step
+    fold is 0 + x / C; equal to numpy's fp64 division bit for bit for x over every binade,
+    zeros, subnormals, the guard's edges, infinities and NaN."""
+    import torch
+    from federated_amd import _lib
+    rng = np.random.default_rng(4343)
+    P = 1 << 21
+    mant = rng.integers(0, 1 << 52, P, dtype=np.uint64)
+    expo = rng.integers(0, 2047, P, dtype=np.uint64)
+    sign = rng.integers(0, 2, P, dtype=np.uint64) << np.uint64(63)
+    x = (sign | (expo << np.uint64(52)) | mant).view(np.float64)
+    edges = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 2.0 ** -900, 2.0 ** 900, -(2.0 ** 900),
+                      np.nextafter(2.0 ** -900, 0.0), np.nextafter(2.0 ** 900, np.inf), 5e-324, 1.7976931348623157e308,
+                      1.0, 3.0])
+    x[:edges.size] = edges
+    xd = torch.from_numpy(x).cuda()
+    zero = torch.zeros(P, dtype=torch.float64, device="cuda")
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    with np.errstate(all="ignore"):
+        for C in divisors:
+            gpu.fold_f64(out, zero, [xd], [1.0], _lib.RULE_SEQUENTIAL_DIV, [C])
+            ref = 0.0 + (1.0 * (x - 0.0)) / C
+            got = out.cpu().numpy()
+            same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+            assert same.all(), (C, x[~same][:4], got[~same][:4], ref[~same][:4])
