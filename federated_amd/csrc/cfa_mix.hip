@@ -61,28 +61,42 @@ __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, lo
   }
 }
 
-// Vector mix + fused compression epilogue (count reduction per block).
+// Vector mix + fused compression epilogue (count reduction per block). Tiles of kBlock * U
+// float4 per block like mix_vec_kernel: U float4 of every stream per lane in flight together
+// (U = 4 while (N + 1) * U <= 40 registers' worth of float4, as auto_vec), nontemporal loads.
 template <int N>
 __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fanin f,
                                                                    long long nvec,
                                                                    CompressParams cp) {
+  constexpr int U = (N + 1) * 4 <= 40 ? 4 : ((N + 1) * 2 <= 40 ? 2 : 1);
+  constexpr long long kTile = (long long)kBlock * U;
   unsigned kept = 0;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
-       i += (long long)gridDim.x * kBlock) {
-    f4 v[N + 1];
+  for (long long base = (long long)blockIdx.x * kTile + threadIdx.x; base < nvec;
+       base += (long long)gridDim.x * kTile) {
+    f4 v[U][N + 1];
 #pragma unroll
-    for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
-    f4 w = fold<N, CFA_RULE_SEQUENTIAL>(v, f);
-    const long long e0 = i * 4;
-    if (e0 + 3 >= cp.cbegin && e0 < cp.cend) {
-      const f4 r = v[0];
+    for (int k = 0; k <= N; ++k)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const long long e = e0 + c;
-        if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
+      for (int u = 0; u < U; ++u) {
+        const long long i = base + (long long)u * kBlock;
+        v[u][k] = i < nvec ? ld4<true>(f.src[k], i) : f4{0.f, 0.f, 0.f, 0.f};
       }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      if (i >= nvec) continue;
+      f4 w = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      const long long e0 = i * 4;
+      if (e0 + 3 >= cp.cbegin && e0 < cp.cend) {
+        const f4 r = v[u][0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const long long e = e0 + c;
+          if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
+        }
+      }
+      st4<true>(out, i, w);
     }
-    st4<false>(out, i, w);
   }
   block_add_count(kept, cp.kept);
 }
@@ -127,12 +141,25 @@ __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float*
                                                           long long nvec, CompressParams cp) {
   unsigned kept = 0;
   const long long stride = (long long)gridDim.x * kBlock;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride) {
-    f4 v = ld4<true>(y, i);
-    const f4 r = ref ? ld4<true>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;  // four float4 of y and ref per lane in flight together
+  constexpr long long kTile = (long long)kBlock * U;
+  for (long long base = (long long)blockIdx.x * kTile + threadIdx.x; base < nvec;
+       base += (long long)gridDim.x * kTile) {
+    f4 v[U], r[U];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = compress_one(v[c], r[c], cp, kept);
-    st4<true>(y, i, v);
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      v[u] = i < nvec ? ld4<true>(y, i) : f4{0.f, 0.f, 0.f, 0.f};
+      r[u] = (i < nvec && ref) ? ld4<true>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      if (i >= nvec) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
+      st4<true>(y, i, v[u]);
+    }
   }
   for (long long i = 4 * nvec + (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += stride) {
     const float r = ref ? ref[i] : 0.0f;
