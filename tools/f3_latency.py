@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """(f3) CFA-GE neighbour-gradient evaluation latency at the driver's shapes
 (federated_sample_CNN_CFA-GE.py / _2NN_CFA-GE.py: 24 samples per device, N = 2 neighbour
-models): the HIP kernel alone (HIP events, one launch for all neighbour models), the host call
+models): the HIP launch alone (HIP events; the drop-in's batch-split launch and the
+one-workgroup-per-model launch), the host call
 (upload, launch, download), torch autograd on the same GPU (vmap over the models), and the
 oracle's numpy float64 evaluation on one core. Prints one JSON line per model kind.
 Usage: python tools/f3_latency.py [--models 2] [--samples 24] [--reps 200]"""
@@ -55,17 +56,26 @@ def main():
         xt, yt = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
         mt = torch.from_numpy(np.stack([np.concatenate([m.reshape(-1) for m in mm]) for mm in models])).cuda()
         gt = torch.empty_like(mt)
-        launch = (lambda: eng.grad_cnn(xt, yt, mt, gt, 16, 8, 5)) if ml == 1 else (lambda: eng.grad_2nn(xt, yt, mt, gt, 32))
-        for _ in range(10):
-            launch()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.reps):
-            launch()
-        e1.record()
-        torch.cuda.synchronize()
-        kernel_us = e0.elapsed_time(e1) * 1e3 / a.reps
+        unsplit = (lambda: eng.grad_cnn(xt, yt, mt, gt, 16, 8, 5)) if ml == 1 else (lambda: eng.grad_2nn(xt, yt, mt, gt, 32))
+        # the drop-in's launch: population form with each model's batch split over workgroups
+        geom = {"filter": 16, "number": 8, "stride": 5} if ml == 1 else {"intermediate_nodes": 32}
+        mrow = torch.arange(M, dtype=torch.int32, device="cuda")
+        drow = torch.zeros(M, dtype=torch.int32, device="cuda")
+        ws = eng.grad_workspace(M, B, P)
+        split = lambda: eng.grad_rows(ml, xt.view(1, B, -1), yt.view(1, B, -1), mt, mrow, drow, gt, geom, workspace=ws)
+
+        def timed(launch):
+            for _ in range(10):
+                launch()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                launch()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / a.reps
+        kernel_us, unsplit_us = timed(split), timed(unsplit)
         T.gradients_batched(ml, x, y, models, stride=5)
         t0 = time.perf_counter()
         for _ in range(a.reps // 4):
@@ -90,7 +100,8 @@ def main():
                 ref(m)
         numpy_us = (time.perf_counter() - t0) / 20 * 1e6
         print(json.dumps({"model": kind, "params": P, "samples": B, "neighbour_models": M,
-                          "hip_kernel_us": round(kernel_us, 2), "hip_host_call_us": round(host_us, 1),
+                          "hip_kernel_us": round(kernel_us, 2), "hip_kernel_unsplit_us": round(unsplit_us, 2),
+                          "batch_splits": eng.grad_splits(M, B, P), "hip_host_call_us": round(host_us, 1),
                           "torch_autograd_vmap_gpu_us": round(torch_us, 1), "numpy_f64_1core_us": round(numpy_us, 1)}),
               flush=True)
 
