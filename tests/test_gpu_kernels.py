@@ -376,7 +376,7 @@ def test_population_kernel_matches_per_device(gpu):
 
 
 def test_full_size_properties(gpu):
-    """BASELINE size (8 neighbours x 25M fp32): exact against the oracle on a sampled window,
+    """BASELINE size (8 neighbours x 25M fp32): exact against the oracle over the whole bucket,
     plus size-independent properties (identity at a=0, convexity bound)."""
     P, n = 25_000_000, 8
     g = torch.Generator(device="cuda").manual_seed(20261015)
@@ -388,9 +388,9 @@ def test_full_size_properties(gpu):
     lo = torch.minimum(local, torch.stack(nbrs).min(0).values)
     hi = torch.maximum(local, torch.stack(nbrs).max(0).values)
     assert bool(((out >= lo - 1e-6) & (out <= hi + 1e-6)).all())
-    sl = slice(12_345_678, 12_345_678 + 65_536)
-    ref = O.sequential_mix(local[sl].cpu().numpy(), [x[sl].cpu().numpy() for x in nbrs], [a] * n)
-    assert np.array_equal(out[sl].cpu().numpy(), ref)
+    # the whole 25M bucket against the oracle, bit for bit (about a second of numpy)
+    ref = O.sequential_mix(local.cpu().numpy(), [x.cpu().numpy() for x in nbrs], [a] * n)
+    assert np.array_equal(out.cpu().numpy(), ref)
     gpu.mix_seq(out, local, nbrs[:1], [0.0])
     assert torch.equal(out, local)
 

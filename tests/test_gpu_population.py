@@ -228,3 +228,23 @@ def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide):
     flat = lambda m: np.concatenate([x.reshape(-1) for x in m])
     if not divide:
         assert np.array_equal(flat(got), sequential_mix(flat(local), [flat(m) for m in nbrs], al))
+
+
+def test_bench_shape_round_full_buckets(gpu):
+    """The bench workload itself (128 devices x 25M fp32, K = 8 ring window, seeded as bench.py
+    seeds them): after one round, the wrap-around devices, the halo-boundary devices and an
+    interior one equal the oracle over their whole 25M buckets, bit for bit."""
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    L, P, h = 128, 25_000_000, 4
+    plan = RingShardPlan(0, 1, L, h)
+    shard = RingPopulationShard(plan, P, torch.device("cuda"), None, gpu)
+    gen = torch.Generator(device="cuda")
+    for i in range(L):
+        gen.manual_seed(20261015 + plan.first + i)
+        shard.models[i].normal_(generator=gen)
+    shard.round()
+    torch.cuda.synchronize()
+    for i in (0, 3, 4, 64, 123, 127):
+        nb = plan.neighbours(i)
+        ref = sequential_mix(shard.models[i].cpu().numpy(), [shard.models[j].cpu().numpy() for j in nb], shard.alphas)
+        assert np.array_equal(shard.mixed[i].cpu().numpy(), ref), i
