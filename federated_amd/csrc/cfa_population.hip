@@ -122,7 +122,7 @@ __device__ __forceinline__ f4 window_fold(const f4* r, int b, const WindowArgs& 
 }
 
 template <int HL, int HR, int U, bool SC1>
-__global__ __launch_bounds__(kBlock) void window_vec_kernel(WindowArgs w, long long nvec) {
+__device__ __forceinline__ void window_body(const WindowArgs& w, long long nvec) {
   constexpr int R = kWinMaxDev + HL + HR;
   constexpr long long kTile = (long long)kBlock * U;
   const int nr = w.nb + HL + HR;
@@ -156,6 +156,43 @@ __global__ __launch_bounds__(kBlock) void window_vec_kernel(WindowArgs w, long l
         }
       }
   }
+}
+
+template <int HL, int HR, int U, bool SC1>
+__global__ __launch_bounds__(kBlock) void window_vec_kernel(WindowArgs w, long long nvec) {
+  window_body<HL, HR, U, SC1>(w, nvec);
+}
+
+// A whole ring-window round of a stacked population in ONE launch (cfa_mix_ring_round_f32):
+// grid.y = pass p over devices [8p, 8p + nb); each block derives its pass's rows from the stack
+// base and pitch (row g of the window = in + ((8p - HL + g) mod D) * pitch), then runs the
+// window pass body. Same operations as one cfa_mix_window_f32 launch per pass.
+struct RingArgs {
+  const float* in;
+  float* out;
+  const float* alphas;  // [D] device array, one coefficient per device
+  long long pitch;      // floats between consecutive devices' rows
+  long long off;        // element offset of this launch's chunk
+  int D;
+};
+
+template <int HL, int HR, int U, bool SC1>
+__global__ __launch_bounds__(kBlock) void ring_round_kernel(RingArgs ra, long long nvec) {
+  const int p = blockIdx.y;
+  WindowArgs w;
+  w.nb = min(kWinMaxDev, ra.D - p * kWinMaxDev);
+#pragma unroll
+  for (int k = 0; k < kWinMaxDev + HL + HR; ++k) {
+    const int g = ((p * kWinMaxDev - HL + k) % ra.D + ra.D) % ra.D;
+    w.rows[k] = ra.in + (long long)g * ra.pitch + ra.off;
+  }
+#pragma unroll
+  for (int b = 0; b < kWinMaxDev; ++b) {
+    const int d = min(p * kWinMaxDev + b, ra.D - 1);
+    w.out[b] = ra.out + (long long)d * ra.pitch + ra.off;
+    w.a[b] = ra.alphas[d];
+  }
+  window_body<HL, HR, U, SC1>(w, nvec);
 }
 
 // Scalar window pass (misaligned rows, the < 4-element tail): runtime hl / hr.
@@ -214,6 +251,39 @@ void launch_window(const WindowArgs& w, long long nvec, hipStream_t st) {
     }
   }
 }
+template <int HL, int HR>
+void launch_ring_round(const RingArgs& ra, long long nvec, hipStream_t st) {
+  const WindowTune t = window_tune();
+  const cfa_launch_t lc{t.blocks_per_cu, t.vec, 1};
+  const unsigned passes = (unsigned)((ra.D + kWinMaxDev - 1) / kWinMaxDev);
+  for (long long done = 0; done < nvec; done += kMaxChunkVec) {
+    const long long m = (nvec - done) < kMaxChunkVec ? (nvec - done) : kMaxChunkVec;
+    RingArgs c = ra;
+    c.off = ra.off + done * 4;
+    const long long tiles = (m + (long long)kBlock * t.vec - 1) / ((long long)kBlock * t.vec);
+    // the launch's blocks over all passes: about blocks_per_cu per CU in all
+    long long gx = (grid_for(tiles, lc) + passes - 1) / passes;
+    if (gx < 1) gx = 1;
+    if (gx > tiles) gx = tiles;
+    const dim3 grid((unsigned)gx, passes);
+    if (t.vec == 1) {
+      if (t.sc1) ring_round_kernel<HL, HR, 1, true><<<grid, kBlock, 0, st>>>(c, m);
+      else ring_round_kernel<HL, HR, 1, false><<<grid, kBlock, 0, st>>>(c, m);
+    } else {
+      if (t.sc1) ring_round_kernel<HL, HR, 2, true><<<grid, kBlock, 0, st>>>(c, m);
+      else ring_round_kernel<HL, HR, 2, false><<<grid, kBlock, 0, st>>>(c, m);
+    }
+  }
+}
+using RingLaunch = void (*)(const RingArgs&, long long, hipStream_t);
+#define CFA_R(L, R) &launch_ring_round<L, R>
+const RingLaunch kRingLaunch[5][5] = {
+    {CFA_R(0, 0), CFA_R(0, 1), CFA_R(0, 2), CFA_R(0, 3), CFA_R(0, 4)},
+    {CFA_R(1, 0), CFA_R(1, 1), CFA_R(1, 2), CFA_R(1, 3), CFA_R(1, 4)},
+    {CFA_R(2, 0), CFA_R(2, 1), CFA_R(2, 2), CFA_R(2, 3), CFA_R(2, 4)},
+    {CFA_R(3, 0), CFA_R(3, 1), CFA_R(3, 2), CFA_R(3, 3), CFA_R(3, 4)},
+    {CFA_R(4, 0), CFA_R(4, 1), CFA_R(4, 2), CFA_R(4, 3), CFA_R(4, 4)}};
+#undef CFA_R
 using WindowLaunch = void (*)(const WindowArgs&, long long, hipStream_t);
 #define CFA_W(L, R) &launch_window<L, R>
 const WindowLaunch kWindowLaunch[5][5] = {
@@ -261,6 +331,24 @@ extern "C" int cfa_mix_window_f32(float* const* out, const float* const* rows, c
     if (int rc = check_launch("window_scalar")) return rc;
   }
   return CFA_OK;
+}
+
+extern "C" int cfa_mix_ring_round_f32(float* out, const float* in, size_t pitch, const float* alphas, int D,
+                                      int hl, int hr, size_t P, void* stream) {
+  if (D < 1) return fail(CFA_E_INVALID, "device count %d", D);
+  if (hl < 0 || hr < 0 || hl > 4 || hr > 4) return fail(CFA_E_INVALID, "window %d/%d outside 0..4", hl, hr);
+  if (hl + hr >= D) return fail(CFA_E_INVALID, "window %d/%d wider than %d devices", hl, hr, D);
+  if (!out || !in || !alphas) return fail(CFA_E_INVALID, "null buffer");
+  if (pitch < P) return fail(CFA_E_INVALID, "pitch %zu below P %zu", pitch, P);
+  if (P == 0) return CFA_OK;
+  if ((addr(out) & 15) || (addr(in) & 15) || (pitch % 4) || (P % 4))
+    return fail(CFA_E_UNSUPPORTED, "ring round needs 16-byte aligned rows (pitch and P multiples of 4)");
+  const long long outb = (long long)addr(out), inb = (long long)addr(in), span = (long long)D * (long long)pitch * 4;
+  if (outb < inb + span && inb < outb + span) return fail(CFA_E_INVALID, "out overlaps in");
+  if ((long long)(D + kWinMaxDev - 1) / kWinMaxDev > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y", D);
+  RingArgs ra{in, out, alphas, (long long)pitch, 0, D};
+  kRingLaunch[hl][hr](ra, (long long)(P / 4), (hipStream_t)stream);
+  return check_launch("ring_round");
 }
 
 extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,

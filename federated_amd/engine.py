@@ -430,6 +430,20 @@ class Engine:
         _lib.call("cfa_mix_window_f32", _lib.ptr_table([o.data_ptr() for o in outs]),
                   _lib.ptr_table([r.data_ptr() for r in rows]), _lib.float_array(per_dev), nb, int(hl), int(hr), P,
                   self.stream_handle(stream))
+    def ring_round(self, out: torch.Tensor, models: torch.Tensor, alphas: torch.Tensor, hl: int, hr: int,
+                   stream=None) -> torch.Tensor:
+        """cfa_mix_ring_round_f32: one launch mixing every device of a stacked [D, P] population
+        with its ring window [d-hl .. d-1, d+1 .. d+hr] (mod D); ``alphas`` [D] fp32 CUDA (one
+        coefficient per device); out [D, P] must not overlap models."""
+        D, P = _check_2d(models, "models")
+        if tuple(out.shape) != (D, P) or not out.is_cuda or out.dtype != torch.float32 or not out.is_contiguous():
+            raise TypeError("out must be a contiguous [D, P] fp32 CUDA tensor")
+        if not alphas.is_cuda or alphas.dtype != torch.float32 or alphas.numel() != D or not alphas.is_contiguous():
+            raise TypeError("alphas must be a contiguous fp32 CUDA tensor of D entries")
+        _lib.call("cfa_mix_ring_round_f32", out.data_ptr(), models.data_ptr(), P, alphas.data_ptr(), D, int(hl),
+                  int(hr), P, self.stream_handle(stream))
+        return out
+
     def ge_population_step(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, state_ptrs: torch.Tensor,
                            grad_ptrs: torch.Tensor, csr_ptr: torch.Tensor, csr_idx: torch.Tensor,
                            csr_coef: torch.Tensor, D: int, rho: float, lr1: float, lr2: float, lr_split: int,

@@ -24,7 +24,11 @@ from ._graphs import RoundGraphs
 from .engine import Engine
 
 RULE_SEQUENTIAL = 0
-WINDOW_MIN_P = 1 << 21  # auto-select window passes above this bucket size
+# auto-select the window round above this bucket size: below it the whole population sits in
+# the 256 MB Infinity Cache and the single CSR launch already reuses rows (tools/probe/
+# window_threshold.py, profiles/r01_window_threshold.jsonl: 32 devices, K = 4: CSR 24.9 vs
+# window 34.5 us at P = 262K; window 73 vs CSR 133 us at 1.07M, 123 vs 256 at 2M)
+WINDOW_MIN_P = 1 << 19
 
 
 # -- neighbour lists for every device ---------------------------------------------------------
@@ -134,10 +138,10 @@ class PopulationRound:
     def set_topology(self, lists, policy, use_window: Optional[bool] = None) -> None:
         """CSR tables for the one-launch population kernel. A ring-window topology with one
         coefficient per device (ring / wrap-around windows under every reference eps policy) can
-        run as cfa_mix_window_f32 passes instead (rows loaded once per 8 devices; same results).
-        ``use_window=None`` picks the passes only for buckets above 2M elements: below that the
-        whole population fits the 256 MB Infinity Cache, the single CSR launch already reuses
-        rows there, and per-pass launch cost dominates (tools/bench_configs.py: C4, C5)."""
+        run as window passes instead (rows loaded once per 8 devices; same results), all in one
+        cfa_mix_ring_round_f32 launch when rows are 16-byte aligned.
+        ``use_window=None`` picks the window round only for buckets above WINDOW_MIN_P (512K
+        elements); below that the CSR launch reuses rows from the Infinity Cache."""
         if use_window is None:
             use_window = self.models.shape[1] > WINDOW_MIN_P
         D = self.models.shape[0]
@@ -147,6 +151,9 @@ class PopulationRound:
         alphas = [list(policy(nb, d, D)) for d, nb in enumerate(lists)]
         shape = window_shape(lists, alphas) if use_window else None
         self.window = (shape[0], shape[1], alphas) if shape else None
+        # one coefficient per device for the one-launch ring round (the window rule has one)
+        self._ring_alphas = (torch.tensor([a[0] if a else 0.0 for a in alphas], dtype=torch.float32, device=dev)
+                             if shape else None)
         self._graphs = None
 
     def run(self, stream=None) -> torch.Tensor:
@@ -160,6 +167,9 @@ class PopulationRound:
         D, P = models.shape
         if self.window is not None:
             hl, hr, alphas = self.window
+            if P % 4 == 0:  # 16-byte rows: every pass in one cfa_mix_ring_round_f32 launch
+                self.engine.ring_round(out, models, self._ring_alphas, hl, hr, stream)
+                return
             for s in range(0, D, 8):
                 devs = list(range(s, min(s + 8, D)))
                 rows = [models[(s + o) % D] for o in range(-hl, len(devs) + hr)]

@@ -238,6 +238,16 @@ CFA_API int cfa_mewma_update_f32(float* W, float* const* s, const float* const* 
 CFA_API int cfa_mix_window_f32(float* const* out, const float* const* rows, const float* alphas,
                                int nb, int hl, int hr, size_t P, void* stream);
 
+/* (e/f4) A whole ring-window round of a STACKED population in one launch: device d's model is
+ * in + d * pitch (P floats), its output out + d * pitch; every device mixes with the ring window
+ * [d-hl .. d-1, d+1 .. d+hr] (mod D) in that order with coefficient alphas[d] (DEVICE array of D
+ * floats) at each step. The devices run as cfa_mix_window_f32 passes of 8 consecutive devices,
+ * all passes in the same launch; results are identical to those passes and to D per-device
+ * sequential mixes. Rows must be 16-byte aligned (pitch and P multiples of 4); out must not
+ * overlap in. */
+CFA_API int cfa_mix_ring_round_f32(float* out, const float* in, size_t pitch, const float* alphas, int D,
+                                   int hl, int hr, size_t P, void* stream);
+
 /* (f3) CFA-GE neighbour-gradient evaluation: the gradient of a device's own cost at each of M
  * neighbour models, for the two TF1 graphs of cfa_ge_2stage.py (:391-433 graph, :512-528 one
  * Session per neighbour; cfa_ge_4stage.py the same), one workgroup per model, fp32 like the

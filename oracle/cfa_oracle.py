@@ -1,9 +1,10 @@
 """ORACLE — TEST INFRASTRUCTURE ONLY. Not part of the product.
 
 CPU (numpy) restatement of the reference's consensus arithmetic, used as the parity checker
-for the HIP kernels in ``libcfa.so``. Only ``tests/``, ``__graft_entry__.smoke()`` and
-``bench.py``'s ``cpu_baseline`` leg may import this module, and only as the checker or as the
-timed CPU baseline. The product path (``federated_amd``) never imports it.
+for the HIP kernels in ``libcfa.so``. Only ``tests/``, ``__graft_entry__.smoke()``,
+``bench.py``'s ``cpu_baseline`` leg and the measurement scripts under ``tools/`` (the numpy
+column of their tables) may import this module, and only as the checker or as the timed CPU
+baseline. The product path (``federated_amd``) never imports it.
 
 Each function restates one reference code path with the same operation order and the same
 numpy dtype rules (numpy 2 / NEP 50 promotion), citing the reference file:line it follows

@@ -182,10 +182,12 @@ def test_window_error_paths(gpu):
         gpu.mix_window([x[10]], x[0:3], [[0.5, 0.25]], 1, 1)
 
 
-@pytest.mark.parametrize("D,P,hl,hr", [(32, 1_071_748 // 8, 2, 2), (128, 24_622, 1, 0), (19, 50_001, 4, 4)])
+@pytest.mark.parametrize("D,P,hl,hr", [(32, 1_071_748 // 8, 2, 2), (128, 24_622, 1, 0), (19, 50_001, 4, 4),
+                                      (32, 1_071_748, 2, 2)])
 def test_population_round_window_path_equals_csr(gpu, D, P, hl, hr):
-    """topology.PopulationRound on a ring window runs cfa_mix_window_f32 passes; identical to
-    the CSR one-launch kernel and to the oracle."""
+    """topology.PopulationRound on a ring window runs the window passes (one
+    cfa_mix_ring_round_f32 launch for 16-byte rows, cfa_mix_window_f32 passes otherwise);
+    identical to the CSR one-launch kernel and to the oracle."""
     from federated_amd import topology as T
     lists = [[(d + o) % D for o in list(range(-hl, 0)) + list(range(1, hr + 1))] for d in range(D)]
     models = torch.randn(D, P, device="cuda")
@@ -248,3 +250,33 @@ def test_bench_shape_round_full_buckets(gpu):
         nb = plan.neighbours(i)
         ref = sequential_mix(shard.models[i].cpu().numpy(), [shard.models[j].cpu().numpy() for j in nb], shard.alphas)
         assert np.array_equal(shard.mixed[i].cpu().numpy(), ref), i
+
+
+@pytest.mark.parametrize("D,hl,hr", [(5, 1, 0), (8, 2, 2), (13, 4, 4), (32, 0, 3), (9, 3, 1)])
+@pytest.mark.parametrize("P", [4, 1000, 4100])
+def test_ring_round_one_launch_equals_per_device(gpu, D, hl, hr, P):
+    """cfa_mix_ring_round_f32 (all window passes of a stacked population in one launch, rows
+    derived from base + pitch with ring wrap-around) equals every device's sequential mix with
+    its window, bit for bit, for partial last passes and one-sided windows too."""
+    g = torch.Generator(device="cuda").manual_seed(D * 1000 + P + 10 * hl + hr)
+    models = torch.randn(D, P, device="cuda", generator=g)
+    out = torch.full((D, P), float("nan"), device="cuda")
+    al = [0.5 / (d + 2) for d in range(D)]
+    gpu.ring_round(out, models, torch.tensor(al, dtype=torch.float32, device="cuda"), hl, hr)
+    torch.cuda.synchronize()
+    h, got = models.cpu().numpy(), out.cpu().numpy()
+    for d in range(D):
+        nb = [(d + o) % D for o in list(range(-hl, 0)) + list(range(1, hr + 1))]
+        assert np.array_equal(got[d], sequential_mix(h[d], [h[j] for j in nb], [al[d]] * len(nb))), d
+
+
+def test_ring_round_rejects_bad_layouts(gpu):
+    from federated_amd import _lib
+    m = torch.zeros(4, 1002, device="cuda")
+    with pytest.raises(_lib.CFAError, match="16-byte"):
+        gpu.ring_round(torch.zeros(4, 1002, device="cuda"), m, torch.zeros(4, device="cuda"), 1, 1)
+    m = torch.zeros(4, 1000, device="cuda")
+    with pytest.raises(_lib.CFAError, match="wider"):
+        gpu.ring_round(torch.zeros(4, 1000, device="cuda"), m, torch.zeros(4, device="cuda"), 2, 2)
+    with pytest.raises(_lib.CFAError, match="overlaps"):
+        gpu.ring_round(m, m, torch.zeros(4, device="cuda"), 1, 1)
