@@ -63,6 +63,57 @@ __global__ __launch_bounds__(kBlock) void population_kernel(float* const* out_pt
   }
 }
 
+// TF1 population round (cfa_mix_population_tf1_f32): per device the numpy-2 chain of the TF1
+// modules (cfa.py:66-76): the first subtraction x_1 - w of two fp32 arrays is fp32, every later
+// operation fp64 with the fp64 coefficients eps * wf_j, one rounding to fp32 at the end. A TF1
+// driver assigns the returned fp64 arrays into its fp32 TF variables, so fp32 buckets mixed this
+// way follow the reference run's trajectory exactly. Same operations as cfa_mix_tf1_f32.
+__global__ __launch_bounds__(kBlock) void population_tf1_kernel(float* const* out_ptrs,
+                                                                const float* const* src_ptrs,
+                                                                const int32_t* csr_ptr,
+                                                                const int32_t* csr_idx,
+                                                                const double* csr_coef,
+                                                                long long nvec, long long P) {
+  const int d = blockIdx.y;
+  const int e0 = csr_ptr[d], e1 = csr_ptr[d + 1];
+  float* out = out_ptrs[d];
+  const float* l = src_ptrs[csr_idx[e0]];
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
+    const f4 lv = ld4<true>(l, i);
+    f4 y = lv;
+    if (e1 - e0 > 1) {
+      const f4 x1 = ld4<true>(src_ptrs[csr_idx[e0 + 1]], i);
+      double w[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float dd = x1[c] - lv[c];                      // fp32 - fp32
+        w[c] = (double)lv[c] + csr_coef[e0 + 1] * (double)dd;  // fp64 from here on
+      }
+      for (int e = e0 + 2; e < e1; ++e) {
+        const f4 x = ld4<true>(src_ptrs[csr_idx[e]], i);
+        const double a = csr_coef[e];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[c] = w[c] + a * ((double)x[c] - w[c]);
+      }
+      y = f4{(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+    }
+    st4<true>(out, i, y);
+  }
+  if (blockIdx.x == 0) {  // the < 4-element tail
+    for (long long i = nvec * 4 + threadIdx.x; i < P; i += kBlock) {
+      const float lv = l[i];
+      float y = lv;
+      if (e1 - e0 > 1) {
+        const float dd = src_ptrs[csr_idx[e0 + 1]][i] - lv;
+        double w = (double)lv + csr_coef[e0 + 1] * (double)dd;
+        for (int e = e0 + 2; e < e1; ++e) w = w + csr_coef[e] * ((double)src_ptrs[csr_idx[e]][i] - w);
+        y = (float)w;
+      }
+      out[i] = y;
+    }
+  }
+}
+
 // Scalar tail for the population kernel (elements [begin, P)).
 template <int RULE>
 __global__ __launch_bounds__(kBlock) void population_tail_kernel(
@@ -349,6 +400,24 @@ extern "C" int cfa_mix_ring_round_f32(float* out, const float* in, size_t pitch,
   RingArgs ra{in, out, alphas, (long long)pitch, 0, D};
   kRingLaunch[hl][hr](ra, (long long)(P / 4), (hipStream_t)stream);
   return check_launch("ring_round");
+}
+
+extern "C" int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                          const int32_t* csr_ptr, const int32_t* csr_idx,
+                                          const double* csr_coef, int D, size_t P, void* stream) {
+  if (D < 0) return fail(CFA_E_INVALID, "negative device count");
+  if (D == 0 || P == 0) return CFA_OK;
+  if (!out_ptrs || !src_ptrs || !csr_ptr || !csr_idx || !csr_coef)
+    return fail(CFA_E_INVALID, "null population table");
+  if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
+  const long long nvec = (long long)P / 4;
+  long long gx = (nvec + kBlock - 1) / kBlock;
+  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  population_tf1_kernel<<<dim3((unsigned)gx, (unsigned)D), kBlock, 0, (hipStream_t)stream>>>(
+      out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, nvec, (long long)P);
+  return check_launch("population_tf1");
 }
 
 extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const* src_ptrs,

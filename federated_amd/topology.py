@@ -82,7 +82,7 @@ def alphas_tf1_ongraphs(eps: float) -> Callable:
     return lambda nbrs, ii, devices: [eps * _tf1.weight_factor(devices, ii, int(j), len(nbrs)) for j in nbrs]
 
 
-def csr(lists: Sequence[Sequence[int]], policy: Callable, devices: Optional[int] = None):
+def csr(lists: Sequence[Sequence[int]], policy: Callable, devices: Optional[int] = None, coef_dtype=np.float32):
     """(ptr, idx, coef) numpy arrays; row d = [d] + lists[d], coef = [1] + alphas."""
     D = len(lists) if devices is None else devices
     ptr, idx, coef = [0], [], []
@@ -91,7 +91,7 @@ def csr(lists: Sequence[Sequence[int]], policy: Callable, devices: Optional[int]
         coef += [1.0] + [float(a) for a in policy(nb, d, D)]
         ptr.append(len(idx))
     return (np.asarray(ptr, dtype=np.int32), np.asarray(idx, dtype=np.int32),
-            np.asarray(coef, dtype=np.float32))
+            np.asarray(coef, dtype=coef_dtype))
 
 
 def window_shape(lists: Sequence[Sequence[int]], alphas: Sequence[Sequence[float]], max_side: int = 4):
@@ -134,18 +134,27 @@ class PopulationRound:
         self.window = None  # (hl, hr, per-device alphas) when the topology is a ring window
         self._graphs: Optional[RoundGraphs] = None  # captured rounds, rebuilt per topology
         self._parity = 0
+        self._tf1 = False
 
-    def set_topology(self, lists, policy, use_window: Optional[bool] = None) -> None:
+    def set_topology(self, lists, policy, use_window: Optional[bool] = None, numerics: str = "fp32") -> None:
         """CSR tables for the one-launch population kernel. A ring-window topology with one
         coefficient per device (ring / wrap-around windows under every reference eps policy) can
         run as window passes instead (rows loaded once per 8 devices; same results), all in one
         cfa_mix_ring_round_f32 launch when rows are 16-byte aligned.
         ``use_window=None`` picks the window round only for buckets above WINDOW_MIN_P (512K
-        elements); below that the CSR launch reuses rows from the Infinity Cache."""
+        elements); below that the CSR launch reuses rows from the Infinity Cache.
+        ``numerics="tf1"``: the TF1 modules' arithmetic (fp32 first subtraction, fp64 chain with
+        the fp64 coefficients, one rounding: cfa_mix_population_tf1_f32), for populations run
+        with ``alphas_tf1_cfa`` / ``alphas_tf1_ongraphs``; "fp32": the TF2 rule."""
+        if numerics not in ("fp32", "tf1"):
+            raise ValueError("numerics must be 'fp32' or 'tf1'")
+        self._tf1 = numerics == "tf1"
         if use_window is None:
             use_window = self.models.shape[1] > WINDOW_MIN_P
+        if self._tf1:
+            use_window = False
         D = self.models.shape[0]
-        ptr, idx, coef = csr(lists, policy, D)
+        ptr, idx, coef = csr(lists, policy, D, np.float64 if self._tf1 else np.float32)
         dev = self.models.device
         self.tables = tuple(torch.from_numpy(a).to(dev) for a in (ptr, idx, coef))
         alphas = [list(policy(nb, d, D)) for d, nb in enumerate(lists)]
@@ -174,6 +183,9 @@ class PopulationRound:
                 devs = list(range(s, min(s + 8, D)))
                 rows = [models[(s + o) % D] for o in range(-hl, len(devs) + hr)]
                 self.engine.mix_window([out[d] for d in devs], rows, [alphas[d] for d in devs], hl, hr, stream)
+            return
+        if self._tf1:
+            self.engine.population_tf1(dst, src, *self.tables, D, P, stream)
             return
         self.engine.population(dst, src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
 
@@ -207,3 +219,75 @@ class PopulationRound:
     def _graph_step(self) -> None:
         self._step_pair(self._parity)
         self._parity ^= 1
+
+
+class Tf1PopulationRound:
+    """A device-resident population on the TF1 protocol (cfa.py:105-154, cfa_ongraphs.py): at
+    epoch e every device mixes its own epoch-e model with the models its neighbours PUBLISHED at
+    epoch e-1 (their pre-mix inputs of e-1, cfa.py:131-139), with the TF1 numerics (fp64 chain,
+    one rounding to fp32: what the driver's fp32 TF variables hold after the assignment).
+
+    Three [D, P] buffers rotate through (current, previous, out): a round mixes current with
+    previous into out, then (current, previous, out) <- (out, current, previous). One
+    ``cfa_mix_population_tf1_f32`` launch per round over the source table [current | previous]."""
+
+    def __init__(self, engine: Engine, D: int, P: int, device=None):
+        dev = engine.device if device is None else torch.device(device)
+        self.engine, self.D, self.P = engine, int(D), int(P)
+        self._bufs = [torch.zeros(self.D, self.P, device=dev) for _ in range(3)]
+        self._rot = 0
+        self._tables = []
+        for r in range(3):
+            cur, prev, out = (self._bufs[(r + k) % 3] for k in range(3))
+            src = torch.tensor([cur[d].data_ptr() for d in range(self.D)] + [prev[d].data_ptr() for d in range(self.D)],
+                               dtype=torch.int64, device=dev)
+            dst = torch.tensor([out[d].data_ptr() for d in range(self.D)], dtype=torch.int64, device=dev)
+            self._tables.append((src, dst))
+        self._csr = None
+        self._graphs: Optional[RoundGraphs] = None
+
+    @property
+    def current(self) -> torch.Tensor:
+        return self._bufs[self._rot]
+
+    @property
+    def previous(self) -> torch.Tensor:
+        return self._bufs[(self._rot + 1) % 3]
+
+    def set_topology(self, lists, policy) -> None:
+        """Neighbour lists and an eps policy (``alphas_tf1_cfa`` / ``alphas_tf1_ongraphs``); the
+        fp64 coefficients go to the device as they are."""
+        D = self.D
+        ptr, idx, coef = [0], [], []
+        for d, nb in enumerate(lists):
+            idx.append(d)
+            coef.append(0.0)
+            idx += [D + int(j) for j in nb]
+            coef += [float(a) for a in policy(nb, d, D)]
+            ptr.append(len(idx))
+        dev = self._bufs[0].device
+        self._csr = (torch.tensor(ptr, dtype=torch.int32, device=dev), torch.tensor(idx, dtype=torch.int32, device=dev),
+                     torch.tensor(coef, dtype=torch.float64, device=dev))
+
+    def load(self, current: torch.Tensor, previous: torch.Tensor) -> None:
+        """current [D, P]: every device's epoch-e model; previous [D, P]: the models published at
+        epoch e-1."""
+        self.current.copy_(current)
+        self.previous.copy_(previous)
+
+    def round(self, stream=None) -> None:
+        if self._csr is None:
+            raise RuntimeError("set_topology() first")
+        src, dst = self._tables[self._rot]
+        self.engine.population_tf1(dst, src, *self._csr, self.D, self.P, stream)
+        self._rot = (self._rot + 2) % 3  # (current, previous, out) <- (out, current, previous)
+
+    def rounds(self, R: int, graph: bool = True) -> None:
+        """R rounds; ``graph=True`` replays captured 3-round periods (hipGraph), same results."""
+        if not graph:
+            for _ in range(R):
+                self.round()
+            return
+        if self._graphs is None:
+            self._graphs = RoundGraphs(self._bufs[0].device, self.round, 3, lambda: self._rot)
+        self._graphs.run(R)

@@ -297,6 +297,16 @@ CFA_API int cfa_mix_population_f32(float* const* out_ptrs, const float* const* s
                            const int32_t* csr_ptr, const int32_t* csr_idx,
                            const float* csr_coef, int D, int rule, size_t P, void* stream);
 
+/* (a1/a2 batched) TF1 population round: as cfa_mix_population_f32 with the TF1 modules'
+ * numerics (cfa.py:66-76 under numpy 2): per device d, w = local; the first neighbour step
+ * subtracts in fp32, every later operation is fp64 with csr_coef[e] (DEVICE double array, the
+ * np.float64 products eps * wf_j; entry e0's coefficient unused), and the result is rounded to
+ * fp32 once: what a TF1 driver's fp32 variables hold after assigning the reference's arrays.
+ * Buckets 16-byte aligned; outputs must not alias any source. */
+CFA_API int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* const* src_ptrs,
+                                       const int32_t* csr_ptr, const int32_t* csr_idx,
+                                       const double* csr_coef, int D, size_t P, void* stream);
+
 /* (a4 batched) CFA-GE population step: stage 1 and the gradient step of every device of a
  * device-resident population in one launch (cfa_ge_2stage.py:446-466, then :591-621). For device
  * d, CSR entries e in [csr_ptr[d], csr_ptr[d+1]): the first is its local model

@@ -77,3 +77,21 @@ def test_cfa_ge_rounds_graph_equals_eager(gpu, ml, pre, R):
     torch.cuda.synchronize()
     for name in ("W", "pub", "S", "G"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize("pre,R", [(0, 3), (1, 8), (2, 13)])
+def test_tf1_population_rounds_graph_equals_eager(gpu, pre, R):
+    from federated_amd import topology as T
+    D, P = 10, 1488
+    g = torch.Generator(device="cuda").manual_seed(77 + pre)
+    cur, prev = torch.randn(D, P, device="cuda", generator=g), torch.randn(D, P, device="cuda", generator=g)
+    a, b = T.Tf1PopulationRound(gpu, D, P), T.Tf1PopulationRound(gpu, D, P)
+    for p in (a, b):
+        p.set_topology(T.kregular_tf1(D, 2), T.alphas_tf1_cfa(0.9, 2))
+        p.load(cur, prev)
+        for _ in range(pre):  # start at another phase of the 3-buffer rotation
+            p.round()
+    a.rounds(R, graph=False)
+    b.rounds(R)
+    torch.cuda.synchronize()
+    assert torch.equal(a.current, b.current) and torch.equal(a.previous, b.previous)

@@ -79,3 +79,42 @@ def test_population_rounds_reproduce_dropin_trajectory(gpu, workdir, version, N,
             assert np.array_equal(got[d], ref), (version, rnd, d)
         pr.models.copy_(out)
     assert sum(sizes) == flat.shape[1]
+
+
+TF1_SHAPES = [(16, 1, 8), (8,), (168, 8), (8,)]  # CFA-GE CNN bucket, P = 1 488 (cfa.py's tensors)
+
+
+@pytest.mark.parametrize("D,N,eps", [(5, 2, 1.0), (8, 3, 0.7)])
+def test_tf1_population_reproduces_dropin_trajectory(gpu, workdir, D, N, eps):
+    """TF1 protocol (cfa.py:105-154): at epoch e every device mixes its epoch-e model with its
+    neighbours' models published at epoch e-1, and the driver assigns the returned fp64 arrays
+    to fp32 TF variables. Four epochs of per-device drop-in calls through the .mat protocol
+    equal Tf1PopulationRound rounds (one cfa_mix_population_tf1_f32 launch each) bit for bit."""
+    from federated_amd import topology as T
+    from federated_amd.consensus.cfa import CFA_process
+    rng = np.random.default_rng(D * 10 + N)
+    sizes = [int(np.prod(s)) for s in TF1_SHAPES]
+    flat = lambda m: np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in m])
+    split = lambda v: [v[o:o + n].reshape(s) for o, n, s in zip(np.cumsum([0] + sizes[:-1]), sizes, TF1_SHAPES)]
+    m0 = [[(rng.standard_normal(s) * 0.1).astype(np.float32) for s in TF1_SHAPES] for _ in range(D)]
+    m1 = [[(rng.standard_normal(s) * 0.1).astype(np.float32) for s in TF1_SHAPES] for _ in range(D)]  # after an SGD step
+    procs = [CFA_process(True, D, d, N) for d in range(D)]
+    for d in range(D):  # epoch 0 publishes
+        W1, b1, W2, b2 = m0[d]
+        procs[d].getFederatedWeight(W1, W2, b1, b2, 0, np.zeros(3), eps)
+    pr = T.Tf1PopulationRound(gpu, D, sum(sizes))
+    pr.set_topology(T.kregular_tf1(D, N), T.alphas_tf1_cfa(eps, N))
+    pr.load(torch.from_numpy(np.stack([flat(m) for m in m1])).cuda(), torch.from_numpy(np.stack([flat(m) for m in m0])).cuda())
+    models = m1
+    for epoch in range(1, 5):
+        new = []
+        for d in range(D):
+            W1, b1, W2, b2 = models[d]
+            out = procs[d].getFederatedWeight(W1, W2, b1, b2, epoch, np.zeros(3), eps)
+            new.append(split(flat([np.float32(a) if np.ndim(a) == 0 else np.asarray(a).astype(np.float32) for a in out])))
+        models = new  # the driver's fp32 TF variables
+        pr.round()
+        torch.cuda.synchronize()
+        got = pr.current.cpu().numpy()
+        for d in range(D):
+            assert np.array_equal(got[d], flat(models[d])), (epoch, d)

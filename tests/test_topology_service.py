@@ -90,3 +90,34 @@ def test_window_shape_detection():
     # step-varying coefficients cannot use the one-alpha-per-device window pass
     lists = win(16, 1, 1)
     assert T.window_shape(lists, [[0.5, 0.25]] * 16) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [200_003, 1_488])
+@pytest.mark.parametrize("rule", ["tf1_cfa", "tf1_ongraphs"])
+def test_population_round_tf1_numerics(gpu, rule, P):
+    """numerics="tf1" (cfa_mix_population_tf1_f32): every device equals fp32 of the reference's
+    numpy-2 chain (oracle.tf1_mix_flat: fp32 first subtraction, fp64 after) and the per-device
+    cfa_mix_tf1_f32 launch, bit for bit; a device without neighbours keeps its model."""
+    from federated_amd import topology as T
+    D = 12
+    models = torch.randn(D, P, device="cuda")
+    pr = T.PopulationRound(gpu, models)
+    if rule == "tf1_cfa":
+        lists, pol = T.kregular_tf1(D, 3), T.alphas_tf1_cfa(0.9, 3)
+    else:
+        lists, pol = T.kregular_tf1(D, 2), T.alphas_tf1_ongraphs(0.8)
+    lists[5] = []
+    pr.set_topology(lists, pol, numerics="tf1")
+    out = pr.run()
+    torch.cuda.synchronize()
+    host = models.cpu().numpy()
+    one = torch.empty(P, device="cuda")
+    for d in range(D):
+        a = pol(lists[d], d, D)
+        ref = np.asarray(O.tf1_mix_flat(host[d], [host[j] for j in lists[d]], a)).astype(np.float32)
+        assert np.array_equal(out[d].cpu().numpy(), ref), (rule, d)
+        if lists[d]:
+            gpu.mix_tf1(one, models[d], [models[j] for j in lists[d]], a)
+            torch.cuda.synchronize()
+            assert torch.equal(one, out[d]), (rule, d)
