@@ -119,6 +119,44 @@ def population(D, P, lists, policy, reps=20, use_window=None):
             "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
 
 
+def tf1_population(D, P, N, eps, rounds=200):
+    """A TF1 cfa.py population resident on the GPU (topology.Tf1PopulationRound: neighbours at
+    epoch e-1, fp64 chain rounded once per round, one launch) against the numpy fp64 chain per
+    device on one core."""
+    eng = get_engine(0)
+    lists, pol = T.kregular_tf1(D, N), T.alphas_tf1_cfa(eps, N)
+    pr = T.Tf1PopulationRound(eng, D, P)
+    pr.set_topology(lists, pol)
+    cur = torch.randn(D, P, device="cuda")
+    pr.load(cur, torch.randn(D, P, device="cuda"))
+    for _ in range(5):
+        pr.round()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(rounds):
+        pr.round()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / rounds * 1e-3
+    pr.rounds(3 * rounds)
+    torch.cuda.synchronize()
+    e0.record()
+    pr.rounds(3 * rounds)
+    e1.record()
+    torch.cuda.synchronize()
+    t_graph = e0.elapsed_time(e1) / (3 * rounds) * 1e-3
+    hc, hp = cur.cpu().numpy(), pr.previous.cpu().numpy()
+
+    def numpy_round():
+        for d in range(D):
+            O.tf1_mix_flat(hc[d], [hp[j] for j in lists[d]], pol(lists[d], d, D))
+    t_np = med_time(numpy_round, 3)
+    return {"devices": D, "P": P, "neighbours": N, "round_us": round(t * 1e6, 1),
+            "round_us_graph": round(t_graph * 1e6, 2), "numpy_fp64_round_ms_1core": round(t_np * 1e3, 3),
+            "speedup_vs_numpy_graph": round(t_np / t_graph, 1)}
+
+
 def _cpu_worker(args):
     seed, P, K, reps = args
     rng = np.random.default_rng(seed)
@@ -216,6 +254,10 @@ def main():
                  **tf1_call([(3, 3, 1, 4), (4,), (4096, 6), (6,)], 8, 3, "ongraphs", compression=2)})
     rows.append({"config": "C3 CFA-GE CNN, 16 devices, N=2 (stage-1 mix via cfa.py math)",
                  **tf1_call([(16, 1, 8), (8,), (168, 8), (8,)], 16, 2, "cfa")})
+    rows.append({"config": "C1 shapes as a device-resident TF1 population (Tf1PopulationRound), 4 devices, N=2",
+                 **tf1_population(4, 16_680, 2, 1.0)})
+    rows.append({"config": "C3 topology as a device-resident TF1 population (stage-1 mix only), 16 devices, N=2",
+                 **tf1_population(16, 1_488, 2, 1.0)})
     rows.append({"config": "C4 CIFAR-100 VGG-1, 32 devices, K=4 window, one population launch",
                  **population(32, 1_071_748, [[(d + o) % 32 for o in (-2, -1, 1, 2)] for d in range(32)], T.alphas_tf2)})
     rows.append({"config": "C5 radar CNN, 128 devices, ring (v4 N=1), one population launch",
