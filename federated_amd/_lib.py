@@ -78,7 +78,7 @@ SIGNATURES = {
     "cfa_mix_ring_round_f32": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_int, _c_int, _c_int,
                                         _c_size_t, _c_void_p]),
     "cfa_mix_population_tf1_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
-                                            _c_size_t, _c_void_p]),
+                                            _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_population_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         _c_int, _c_int, _c_size_t, _c_void_p]),
     "cfa_ge_grad_cnn_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,

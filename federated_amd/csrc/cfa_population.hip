@@ -73,15 +73,31 @@ __global__ __launch_bounds__(kBlock) void population_tf1_kernel(float* const* ou
                                                                 const int32_t* csr_ptr,
                                                                 const int32_t* csr_idx,
                                                                 const double* csr_coef,
-                                                                long long nvec, long long P) {
+                                                                long long nvec, long long P,
+                                                                CompressParams cp) {
   const int d = blockIdx.y;
   const int e0 = csr_ptr[d], e1 = csr_ptr[d + 1];
   float* out = out_ptrs[d];
   const float* l = src_ptrs[csr_idx[e0]];
+  unsigned kept = 0;
+  // the compression epilogue (cfa_ongraphs.py:225-273) on [cbegin, cend): fp64 against the
+  // pre-mix local after a mix, fp32 on the local itself for a device without neighbours (the
+  // reference then compresses the caller's fp32 array in place, numpy-2 fp32 thresholds)
+  auto epi = [&](double w, float lv, long long e) -> float {
+    if (cp.mode && e >= cp.cbegin && e < cp.cend) return (float)compress_one_d(w, (double)lv, cp, kept);
+    return (float)w;
+  };
+  auto epi0 = [&](float lv, long long e) -> float {
+    if (cp.mode && e >= cp.cbegin && e < cp.cend) return compress_one(lv, lv, cp, kept);
+    return lv;
+  };
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
     const f4 lv = ld4<true>(l, i);
-    f4 y = lv;
-    if (e1 - e0 > 1) {
+    f4 y;
+    if (e1 - e0 <= 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) y[c] = epi0(lv[c], 4 * i + c);
+    } else {
       const f4 x1 = ld4<true>(src_ptrs[csr_idx[e0 + 1]], i);
       double w[4];
 #pragma unroll
@@ -95,23 +111,27 @@ __global__ __launch_bounds__(kBlock) void population_tf1_kernel(float* const* ou
 #pragma unroll
         for (int c = 0; c < 4; ++c) w[c] = w[c] + a * ((double)x[c] - w[c]);
       }
-      y = f4{(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) y[c] = epi(w[c], lv[c], 4 * i + c);
     }
     st4<true>(out, i, y);
   }
   if (blockIdx.x == 0) {  // the < 4-element tail
     for (long long i = nvec * 4 + threadIdx.x; i < P; i += kBlock) {
       const float lv = l[i];
-      float y = lv;
-      if (e1 - e0 > 1) {
+      float y;
+      if (e1 - e0 <= 1) {
+        y = epi0(lv, i);
+      } else {
         const float dd = src_ptrs[csr_idx[e0 + 1]][i] - lv;
         double w = (double)lv + csr_coef[e0 + 1] * (double)dd;
         for (int e = e0 + 2; e < e1; ++e) w = w + csr_coef[e] * ((double)src_ptrs[csr_idx[e]][i] - w);
-        y = (float)w;
+        y = epi(w, lv, i);
       }
       out[i] = y;
     }
   }
+  if (cp.mode) block_add_count(kept, cp.kept + d);
 }
 
 // Scalar tail for the population kernel (elements [begin, P)).
@@ -404,8 +424,17 @@ extern "C" int cfa_mix_ring_round_f32(float* out, const float* in, size_t pitch,
 
 extern "C" int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* const* src_ptrs,
                                           const int32_t* csr_ptr, const int32_t* csr_idx,
-                                          const double* csr_coef, int D, size_t P, void* stream) {
+                                          const double* csr_coef, int D, size_t P, int mode,
+                                          size_t cbegin, size_t cend, unsigned long long* kept_counts,
+                                          void* stream) {
   if (D < 0) return fail(CFA_E_INVALID, "negative device count");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  if (mode && (!kept_counts || cbegin > cend || cend > P))
+    return fail(CFA_E_INVALID, "compression needs per-device counters and a segment within the bucket");
+  cp.cbegin = (long long)cbegin;
+  cp.cend = (long long)cend;
+  cp.kept = kept_counts;
   if (D == 0 || P == 0) return CFA_OK;
   if (!out_ptrs || !src_ptrs || !csr_ptr || !csr_idx || !csr_coef)
     return fail(CFA_E_INVALID, "null population table");
@@ -416,7 +445,7 @@ extern "C" int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* c
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   population_tf1_kernel<<<dim3((unsigned)gx, (unsigned)D), kBlock, 0, (hipStream_t)stream>>>(
-      out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, nvec, (long long)P);
+      out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, nvec, (long long)P, cp);
   return check_launch("population_tf1");
 }
 

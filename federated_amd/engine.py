@@ -476,9 +476,13 @@ class Engine:
                   int(r_M), int(r_sp), self.stream_handle(stream))
 
     def population_tf1(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
-                       csr_idx: torch.Tensor, csr_coef64: torch.Tensor, D: int, P: int, stream=None) -> None:
+                       csr_idx: torch.Tensor, csr_coef64: torch.Tensor, D: int, P: int, stream=None,
+                       mode: int = 0, cbegin: int = 0, cend: int = 0,
+                       kept: Optional[torch.Tensor] = None) -> None:
         """One launch mixing D devices with the TF1 numerics (cfa_mix_population_tf1_f32):
-        fp32 first subtraction, fp64 chain with fp64 coefficients, one rounding to fp32."""
+        fp32 first subtraction, fp64 chain with fp64 coefficients, one rounding to fp32.
+        ``mode`` != 0: the compression epilogue on [cbegin, cend) of every device, counts added
+        to ``kept`` (int64 CUDA tensor of D zeroed counters)."""
         for name, t, dt in (("out_ptrs", out_ptrs, torch.int64), ("src_ptrs", src_ptrs, torch.int64),
                             ("csr_ptr", csr_ptr, torch.int32), ("csr_idx", csr_idx, torch.int32),
                             ("csr_coef64", csr_coef64, torch.float64)):
@@ -486,8 +490,11 @@ class Engine:
                 raise TypeError(f"{name} must be a contiguous {dt} CUDA tensor")
         if csr_ptr.numel() != D + 1 or out_ptrs.numel() != D:
             raise ValueError("csr_ptr must have D+1 entries and out_ptrs D entries")
+        if mode and (kept is None or not kept.is_cuda or kept.dtype != torch.int64 or kept.numel() != D):
+            raise TypeError("compression needs kept: an int64 CUDA tensor of D counters")
         _lib.call("cfa_mix_population_tf1_f32", out_ptrs.data_ptr(), src_ptrs.data_ptr(), csr_ptr.data_ptr(),
-                  csr_idx.data_ptr(), csr_coef64.data_ptr(), int(D), int(P), self.stream_handle(stream))
+                  csr_idx.data_ptr(), csr_coef64.data_ptr(), int(D), int(P), int(mode), int(cbegin), int(cend),
+                  kept.data_ptr() if kept is not None else None, self.stream_handle(stream))
 
     def population(self, out_ptrs: torch.Tensor, src_ptrs: torch.Tensor, csr_ptr: torch.Tensor,
                    csr_idx: torch.Tensor, csr_coef: torch.Tensor, D: int, rule: int, P: int,

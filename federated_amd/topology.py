@@ -14,7 +14,7 @@ the same RNG calls) and the same per-step alphas, so one launch reproduces D per
 from __future__ import annotations
 
 import random
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -136,7 +136,8 @@ class PopulationRound:
         self._parity = 0
         self._tf1 = False
 
-    def set_topology(self, lists, policy, use_window: Optional[bool] = None, numerics: str = "fp32") -> None:
+    def set_topology(self, lists, policy, use_window: Optional[bool] = None, numerics: str = "fp32",
+                     compression: Optional[Tuple[int, int, int]] = None) -> None:
         """CSR tables for the one-launch population kernel. A ring-window topology with one
         coefficient per device (ring / wrap-around windows under every reference eps policy) can
         run as window passes instead (rows loaded once per 8 devices; same results), all in one
@@ -145,10 +146,17 @@ class PopulationRound:
         elements); below that the CSR launch reuses rows from the Infinity Cache.
         ``numerics="tf1"``: the TF1 modules' arithmetic (fp32 first subtraction, fp64 chain with
         the fp64 coefficients, one rounding: cfa_mix_population_tf1_f32), for populations run
-        with ``alphas_tf1_cfa`` / ``alphas_tf1_ongraphs``; "fp32": the TF2 rule."""
+        with ``alphas_tf1_cfa`` / ``alphas_tf1_ongraphs``; "fp32": the TF2 rule.
+        ``compression=(mode, cbegin, cend)`` (TF1 numerics only): the cfa_ongraphs epilogue on
+        every device's [cbegin, cend) segment; ``kept`` then holds each device's counter_param
+        after a round."""
         if numerics not in ("fp32", "tf1"):
             raise ValueError("numerics must be 'fp32' or 'tf1'")
         self._tf1 = numerics == "tf1"
+        if compression is not None and not self._tf1:
+            raise ValueError("the compression epilogue belongs to the TF1 (cfa_ongraphs) numerics")
+        self._compress = tuple(int(v) for v in compression) if compression else (0, 0, 0)
+        self.kept = torch.zeros(self.models.shape[0], dtype=torch.int64, device=self.models.device)
         if use_window is None:
             use_window = self.models.shape[1] > WINDOW_MIN_P
         if self._tf1:
@@ -185,7 +193,10 @@ class PopulationRound:
                 self.engine.mix_window([out[d] for d in devs], rows, [alphas[d] for d in devs], hl, hr, stream)
             return
         if self._tf1:
-            self.engine.population_tf1(dst, src, *self.tables, D, P, stream)
+            mode, cb, ce = self._compress
+            if mode:
+                self.kept.zero_()
+            self.engine.population_tf1(dst, src, *self.tables, D, P, stream, mode, cb, ce, self.kept if mode else None)
             return
         self.engine.population(dst, src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
 
@@ -245,6 +256,8 @@ class Tf1PopulationRound:
             self._tables.append((src, dst))
         self._csr = None
         self._graphs: Optional[RoundGraphs] = None
+        self._compress = (0, 0, 0)
+        self.kept = torch.zeros(self.D, dtype=torch.int64, device=dev)
 
     @property
     def current(self) -> torch.Tensor:
@@ -254,9 +267,12 @@ class Tf1PopulationRound:
     def previous(self) -> torch.Tensor:
         return self._bufs[(self._rot + 1) % 3]
 
-    def set_topology(self, lists, policy) -> None:
+    def set_topology(self, lists, policy, compression: Optional[Tuple[int, int, int]] = None) -> None:
         """Neighbour lists and an eps policy (``alphas_tf1_cfa`` / ``alphas_tf1_ongraphs``); the
-        fp64 coefficients go to the device as they are."""
+        fp64 coefficients go to the device as they are. ``compression=(mode, cbegin, cend)``:
+        the cfa_ongraphs epilogue on every device's [cbegin, cend) (its W2 segment); ``kept``
+        holds each device's counter_param after a round."""
+        self._compress = tuple(int(v) for v in compression) if compression else (0, 0, 0)
         D = self.D
         ptr, idx, coef = [0], [], []
         for d, nb in enumerate(lists):
@@ -279,7 +295,11 @@ class Tf1PopulationRound:
         if self._csr is None:
             raise RuntimeError("set_topology() first")
         src, dst = self._tables[self._rot]
-        self.engine.population_tf1(dst, src, *self._csr, self.D, self.P, stream)
+        mode, cb, ce = self._compress
+        if mode:
+            self.kept.zero_()
+        self.engine.population_tf1(dst, src, *self._csr, self.D, self.P, stream, mode, cb, ce,
+                                   self.kept if mode else None)
         self._rot = (self._rot + 2) % 3  # (current, previous, out) <- (out, current, previous)
 
     def rounds(self, R: int, graph: bool = True) -> None:

@@ -302,10 +302,15 @@ CFA_API int cfa_mix_population_f32(float* const* out_ptrs, const float* const* s
  * subtracts in fp32, every later operation is fp64 with csr_coef[e] (DEVICE double array, the
  * np.float64 products eps * wf_j; entry e0's coefficient unused), and the result is rounded to
  * fp32 once: what a TF1 driver's fp32 variables hold after assigning the reference's arrays.
- * Buckets 16-byte aligned; outputs must not alias any source. */
+ * mode != CFA_COMPRESS_NONE: the cfa_ongraphs compression epilogue (cfa_ongraphs.py:225-273)
+ * on elements [cbegin, cend) of every device (the W2 segment), against the device's pre-mix
+ * local, before the rounding, as cfa_mix_tf1_f32 applies it; a device without neighbours gets
+ * the fp32 epilogue on its local. kept_counts[d] (DEVICE, D counters, zeroed by the caller)
+ * += device d's counter_param. Buckets 16-byte aligned; outputs must not alias any source. */
 CFA_API int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* const* src_ptrs,
                                        const int32_t* csr_ptr, const int32_t* csr_idx,
-                                       const double* csr_coef, int D, size_t P, void* stream);
+                                       const double* csr_coef, int D, size_t P, int mode, size_t cbegin,
+                                       size_t cend, unsigned long long* kept_counts, void* stream);
 
 /* (a4 batched) CFA-GE population step: stage 1 and the gradient step of every device of a
  * device-resident population in one launch (cfa_ge_2stage.py:446-466, then :591-621). For device

@@ -121,3 +121,34 @@ def test_population_round_tf1_numerics(gpu, rule, P):
             gpu.mix_tf1(one, models[d], [models[j] for j in lists[d]], a)
             torch.cuda.synchronize()
             assert torch.equal(one, out[d]), (rule, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_population_round_tf1_compression(gpu, mode):
+    """BASELINE config 2 as one population launch: FL_CFA_CNN_tf2 buckets (P = 24 622, W2 =
+    elements [44, 24620)), 8 devices, 3 neighbours, the cfa_ongraphs alpha eps/(1+n), and the
+    compression epilogue on W2 (cfa_ongraphs.py:225-273). Every device equals the per-device
+    cfa_mix_tf1_f32 launch bit for bit, counter_param included; a device without neighbours gets
+    the fp32 epilogue on its own model, as the reference compresses the caller's array."""
+    from federated_amd import topology as T
+    D, P, cb, ce = 8, 24_624, 44, 44 + 4096 * 6
+    g = torch.Generator(device="cuda").manual_seed(mode)
+    scale = {1: 1e-3, 2: 1e-4, 3: 1e-3, 4: 1e-2}[mode]  # weights near each mode's threshold
+    models = torch.randn(D, P, device="cuda", generator=g) * scale
+    lists = [[(d + o) % D for o in (-1, 1, 2)] for d in range(D)]
+    lists[3] = []
+    pol = T.alphas_tf1_ongraphs(0.8)
+    pr = T.PopulationRound(gpu, models)
+    pr.set_topology(lists, pol, numerics="tf1", compression=(mode, cb, ce))
+    out = pr.run()
+    torch.cuda.synchronize()
+    one = torch.empty(P, device="cuda")
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for d in range(D):
+        kept.zero_()
+        gpu.mix_tf1(one, models[d], [models[j] for j in lists[d]], pol(lists[d], d, D), mode, cb, ce, kept)
+        torch.cuda.synchronize()
+        assert torch.equal(one, out[d]), (mode, d)
+        assert int(kept.item()) == int(pr.kept[d].item()), (mode, d)
+    assert 0 < int(pr.kept.sum().item()) < D * (ce - cb)

@@ -119,14 +119,16 @@ def population(D, P, lists, policy, reps=20, use_window=None):
             "numpy_round_ms_1core": round(t_np * 1e3, 2), "speedup_vs_numpy": round(t_np / t, 1)}
 
 
-def tf1_population(D, P, N, eps, rounds=200):
+def tf1_population(D, P, N, eps, rounds=200, compression=None):
     """A TF1 cfa.py population resident on the GPU (topology.Tf1PopulationRound: neighbours at
     epoch e-1, fp64 chain rounded once per round, one launch) against the numpy fp64 chain per
-    device on one core."""
+    device on one core. ``compression=(mode, cbegin, cend)``: the cfa_ongraphs alpha eps/(1+n)
+    and its compression epilogue (numpy: oracle.tf1_compress on the W2 segment)."""
     eng = get_engine(0)
-    lists, pol = T.kregular_tf1(D, N), T.alphas_tf1_cfa(eps, N)
+    lists = T.kregular_tf1(D, N)
+    pol = T.alphas_tf1_ongraphs(eps) if compression else T.alphas_tf1_cfa(eps, N)
     pr = T.Tf1PopulationRound(eng, D, P)
-    pr.set_topology(lists, pol)
+    pr.set_topology(lists, pol, compression=compression)
     cur = torch.randn(D, P, device="cuda")
     pr.load(cur, torch.randn(D, P, device="cuda"))
     for _ in range(5):
@@ -150,7 +152,10 @@ def tf1_population(D, P, N, eps, rounds=200):
 
     def numpy_round():
         for d in range(D):
-            O.tf1_mix_flat(hc[d], [hp[j] for j in lists[d]], pol(lists[d], d, D))
+            w = O.tf1_mix_flat(hc[d], [hp[j] for j in lists[d]], pol(lists[d], d, D))
+            if compression:
+                mode, cb, ce = compression
+                O.tf1_compress(np.array(w[cb:ce]), hc[d][cb:ce], mode)
     t_np = med_time(numpy_round, 3)
     return {"devices": D, "P": P, "neighbours": N, "round_us": round(t * 1e6, 1),
             "round_us_graph": round(t_graph * 1e6, 2), "numpy_fp64_round_ms_1core": round(t_np * 1e3, 3),
@@ -258,6 +263,9 @@ def main():
                  **tf1_population(4, 16_680, 2, 1.0)})
     rows.append({"config": "C3 topology as a device-resident TF1 population (stage-1 mix only), 16 devices, N=2",
                  **tf1_population(16, 1_488, 2, 1.0)})
+    rows.append({"config": "C2 as a device-resident TF1 population: FL_CFA_CNN_tf2 buckets, 8 devices, K=3, "
+                           "cfa_ongraphs mode 1 alpha, compression 2 on W2",
+                 **tf1_population(8, 24_622, 3, 1.0, compression=(2, 40, 40 + 4096 * 6))})
     rows.append({"config": "C4 CIFAR-100 VGG-1, 32 devices, K=4 window, one population launch",
                  **population(32, 1_071_748, [[(d + o) % 32 for o in (-2, -1, 1, 2)] for d in range(32)], T.alphas_tf2)})
     rows.append({"config": "C5 radar CNN, 128 devices, ring (v4 N=1), one population launch",
