@@ -118,3 +118,54 @@ def test_tf1_population_reproduces_dropin_trajectory(gpu, workdir, D, N, eps):
         got = pr.current.cpu().numpy()
         for d in range(D):
             assert np.array_equal(got[d], flat(models[d])), (epoch, d)
+
+
+ONGRAPHS_SHAPES = [(3, 3, 1, 4), (4,), (4096, 6), (6,)]  # FL_CFA_CNN_tf2.py:56-65, P = 24 622
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+def test_tf1_ongraphs_population_with_compression_reproduces_dropin(gpu, workdir, mode):
+    """Config 2's protocol (FL_CFA_CNN_tf2.py:253-266): per epoch a cfa_ongraphs consensus_mode 1
+    call mixes all neighbours' epoch e-1 files (alpha = eps/(1+n)) with the DPCM compression
+    epilogue on W2, then a stop_consensus call with no neighbours publishes the fp32 result (its
+    DPCM pass against itself changes no value). The published model is thus the post-mix one,
+    so without SGD in between every device mixes the current models: three epochs of these
+    per-device calls equal three PopulationRound(numerics="tf1", compression=...) rounds bit for
+    bit, outputs and every device's counter_param. (The sparse modes 1/4 also re-compress at
+    publish time, in fp32; a population round does not model that second pass.)"""
+    from federated_amd import topology as T
+    from federated_amd.consensus.cfa_ongraphs import CFA_process
+    D, N, eps = 8, 3, 1.0
+    rng = np.random.default_rng(40 + mode)
+    sizes = [int(np.prod(s)) for s in ONGRAPHS_SHAPES]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    flat = lambda m: np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in m])
+    split = lambda v: [v[offs[k]:offs[k + 1]].reshape(s) for k, s in enumerate(ONGRAPHS_SHAPES)]
+    scale = 1e-4 if mode == 2 else 1e-3  # weights near the mode's threshold (DPCM differences)
+    models = [[(rng.standard_normal(s) * scale).astype(np.float32) for s in ONGRAPHS_SHAPES] for _ in range(D)]
+    lists = T.kregular_tf1(D, N)
+    procs = [CFA_process(True, D, d, N, 1, mode, 1) for d in range(D)]  # graph 1: the passed lists
+    for d in range(D):
+        W1, b1, W2, b2 = models[d]
+        procs[d].getFederatedWeight(W1, W2, b1, b2, 0, np.zeros(3), eps, [], False)
+    pop = torch.from_numpy(np.stack([flat(m) for m in models])).cuda()
+    pr = T.PopulationRound(gpu, pop)
+    pr.set_topology(lists, T.alphas_tf1_ongraphs(eps), numerics="tf1", compression=(mode, int(offs[2]), int(offs[3])))
+    for epoch in range(1, 4):
+        new, counts = [], []
+        for d in range(D):
+            W1, b1, W2, b2 = (np.array(a) for a in models[d])
+            res = procs[d].getFederatedWeight(W1, W2, b1, b2, epoch, np.zeros(3), eps, list(lists[d]), False)
+            counts.append(int(res[4]))
+            nxt = split(flat(res[:4]))  # the driver's fp32 variables
+            procs[d].getFederatedWeight(nxt[0], nxt[2], nxt[1], nxt[3], epoch, np.zeros(3), eps, [], True)
+            new.append(nxt)
+        models = new
+        out = pr.run()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for d in range(D):
+            assert np.array_equal(got[d], flat(models[d])), (epoch, d)
+        assert pr.kept.cpu().tolist() == counts, epoch
+        assert 0 < sum(counts) < D * sizes[2]
+        pop.copy_(out)
