@@ -120,17 +120,25 @@ def population(D, P, lists, policy, reps=20, use_window=None):
 
 
 def tf1_population(D, P, N, eps, rounds=200, compression=None):
-    """A TF1 cfa.py population resident on the GPU (topology.Tf1PopulationRound: neighbours at
-    epoch e-1, fp64 chain rounded once per round, one launch) against the numpy fp64 chain per
-    device on one core. ``compression=(mode, cbegin, cend)``: the cfa_ongraphs alpha eps/(1+n)
-    and its compression epilogue (numpy: oracle.tf1_compress on the W2 segment)."""
+    """A TF1 population resident on the GPU against the numpy fp64 chain per device on one core:
+    cfa.py (topology.Tf1PopulationRound: neighbours at epoch e-1), or with ``compression=(mode,
+    cbegin, cend)`` cfa_ongraphs mode 1 (PopulationRound(numerics="tf1"): alpha eps/(1+n), the
+    compression epilogue; numpy: oracle.tf1_compress on the W2 segment). One launch per round,
+    fp64 chain rounded once."""
     eng = get_engine(0)
     lists = T.kregular_tf1(D, N)
-    pol = T.alphas_tf1_ongraphs(eps) if compression else T.alphas_tf1_cfa(eps, N)
-    pr = T.Tf1PopulationRound(eng, D, P)
-    pr.set_topology(lists, pol, compression=compression)
     cur = torch.randn(D, P, device="cuda")
-    pr.load(cur, torch.randn(D, P, device="cuda"))
+    if compression:
+        # cfa_ongraphs mode 1 publishes the post-mix model: neighbours are the current models
+        pol = T.alphas_tf1_ongraphs(eps)
+        pr = T.PopulationRound(eng, cur)
+        pr.set_topology(lists, pol, numerics="tf1", compression=compression)
+        pr.round, pr.previous = pr.run, cur
+    else:
+        pol = T.alphas_tf1_cfa(eps, N)
+        pr = T.Tf1PopulationRound(eng, D, P)
+        pr.set_topology(lists, pol)
+        pr.load(cur, torch.randn(D, P, device="cuda"))
     for _ in range(5):
         pr.round()
     torch.cuda.synchronize()
