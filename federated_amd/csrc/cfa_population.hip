@@ -14,7 +14,7 @@ __global__ __launch_bounds__(kBlock) void population_kernel(float* const* out_pt
                                                             const int32_t* csr_ptr,
                                                             const int32_t* csr_idx,
                                                             const float* csr_coef,
-                                                            long long nvec) {
+                                                            long long nvec, long long P) {
   const int d = blockIdx.y;
   const int e0 = csr_ptr[d];
   const int e1 = csr_ptr[d + 1];
@@ -60,6 +60,25 @@ __global__ __launch_bounds__(kBlock) void population_kernel(float* const* out_pt
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (ok[u]) st4<true>(out, idx[u], w[u]);
+  }
+  // the < 4-element tail, in the same launch (one kernel boundary fewer per round): the
+  // scalar form of the same operations, so every element rounds as in the float4 body
+  if (blockIdx.x == 0 && nvec * 4 + threadIdx.x < P) {
+    const long long i = nvec * 4 + threadIdx.x;
+    float w = src_ptrs[csr_idx[e0]][i];
+    if constexpr (RULE == CFA_RULE_LINEAR) w = csr_coef[e0] * w;
+    for (int e = e0 + 1; e < e1; ++e) {
+      const float x = src_ptrs[csr_idx[e]][i];
+      const float c = csr_coef[e];
+      if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
+        float tt = x - w;
+        tt = c * tt;
+        w = w + tt;
+      } else {
+        w = fmaf(c, x, w);
+      }
+    }
+    out[i] = w;
   }
 }
 
@@ -132,31 +151,6 @@ __global__ __launch_bounds__(kBlock) void population_tf1_kernel(float* const* ou
     }
   }
   if (cp.mode) block_add_count(kept, cp.kept + d);
-}
-
-// Scalar tail for the population kernel (elements [begin, P)).
-template <int RULE>
-__global__ __launch_bounds__(kBlock) void population_tail_kernel(
-    float* const* out_ptrs, const float* const* src_ptrs, const int32_t* csr_ptr,
-    const int32_t* csr_idx, const float* csr_coef, long long begin, long long P) {
-  const int d = blockIdx.y;
-  const long long i = begin + threadIdx.x;
-  if (i >= P) return;
-  const int e0 = csr_ptr[d], e1 = csr_ptr[d + 1];
-  float w = src_ptrs[csr_idx[e0]][i];
-  if constexpr (RULE == CFA_RULE_LINEAR) w = csr_coef[e0] * w;
-  for (int e = e0 + 1; e < e1; ++e) {
-    const float x = src_ptrs[csr_idx[e]][i];
-    const float c = csr_coef[e];
-    if constexpr (RULE == CFA_RULE_SEQUENTIAL) {
-      float tt = x - w;
-      tt = c * tt;
-      w = w + tt;
-    } else {
-      w = fmaf(c, x, w);
-    }
-  }
-  out_ptrs[d][i] = w;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -462,33 +456,20 @@ extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const
   if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
   hipStream_t st = (hipStream_t)stream;
   // Buckets in a population are expected 16-byte aligned (allocator contract, checked by the
-  // host layer); the body runs on float4, the <4-element tail on the scalar kernel.
+  // host layer); the body runs on float4, the <4-element tail in the first tile column.
   const long long nvec = (long long)P / 4;
-  if (nvec > 0) {
-    const long long tiles = (nvec + 2LL * kBlock - 1) / (2LL * kBlock);
-    long long gx = tiles;
-    const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
-    if (gx > cap) gx = cap < 1 ? 1 : cap;
-    dim3 grid((unsigned)gx, (unsigned)D);
-    if (rule == CFA_RULE_SEQUENTIAL)
-      population_kernel<CFA_RULE_SEQUENTIAL><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
-                                                                      csr_idx, csr_coef, nvec);
-    else
-      population_kernel<CFA_RULE_LINEAR><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
-                                                                  csr_idx, csr_coef, nvec);
-    if (int rc = check_launch("population")) return rc;
-  }
-  const long long begin = nvec * 4;
-  if (begin < (long long)P) {
-    dim3 grid(1, (unsigned)D);
-    if (rule == CFA_RULE_SEQUENTIAL)
-      population_tail_kernel<CFA_RULE_SEQUENTIAL><<<grid, 64, 0, st>>>(
-          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
-    else
-      population_tail_kernel<CFA_RULE_LINEAR><<<grid, 64, 0, st>>>(
-          out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, begin, (long long)P);
-    if (int rc = check_launch("population_tail")) return rc;
-  }
+  long long gx = (nvec + 2LL * kBlock - 1) / (2LL * kBlock);
+  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  dim3 grid((unsigned)gx, (unsigned)D);
+  if (rule == CFA_RULE_SEQUENTIAL)
+    population_kernel<CFA_RULE_SEQUENTIAL><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                    csr_idx, csr_coef, nvec, (long long)P);
+  else
+    population_kernel<CFA_RULE_LINEAR><<<grid, kBlock, 0, st>>>(out_ptrs, src_ptrs, csr_ptr,
+                                                                csr_idx, csr_coef, nvec, (long long)P);
+  if (int rc = check_launch("population")) return rc;
   return CFA_OK;
 }
 

@@ -111,6 +111,25 @@ def test_config_shapes_population_kernel(gpu, name, D, P, nbr_fn, alpha_fn):
         assert np.array_equal(outs[i].cpu().numpy(), ref), (name, i)
 
 
+@pytest.mark.parametrize("P", [1, 3, 4, 6, 1029, 2 * 256 * 4 + 3])
+def test_population_kernel_small_and_ragged(gpu, P):
+    """Buckets with no float4 body (P < 4) and ragged tails: the scalar tail runs inside the
+    population launch (first tile column) and must round like the float4 body."""
+    D = 5
+    g = torch.Generator(device="cuda").manual_seed(P)
+    buckets = [torch.randn(P, generator=g, device="cuda") for _ in range(D)]
+    outs = [torch.empty(P, device="cuda") for _ in range(D)]
+    nbr_fn = lambda i: [(i + o) % D for o in (-1, 1, 2)]
+    alpha_fn = lambda n: [1.0 / (n + 1)] * n
+    tables = _pop_tables(D, nbr_fn, alpha_fn, buckets, outs)
+    gpu.population(*tables, D, 0, P)
+    torch.cuda.synchronize()
+    host = [b.cpu().numpy() for b in buckets]
+    for i in range(D):
+        ref = sequential_mix(host[i], [host[j] for j in nbr_fn(i)], alpha_fn(3))
+        assert np.array_equal(outs[i].cpu().numpy(), ref), (P, i)
+
+
 def test_config5_ring_round_world1(gpu):
     """Config 5 topology through the shard round (one-sided ring window)."""
     from federated_amd.population import RingPopulationShard, RingShardPlan
