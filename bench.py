@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import statistics
 import os
 import platform
 import sys
@@ -272,6 +273,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "avg_launch_ms": round(avg_ms, 5),
+                "step_avg_launch_ms_median": round(statistics.median(durations), 5) if durations else None,
+                "step_avg_launch_ms_min": round(min(durations), 5) if durations else None,
                 "launches_timed": launches_timed,
                 "timing": "HIP events around each step's back-to-back interior mixes / launches",
                 "traffic": load_traffic(
