@@ -279,3 +279,60 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_free(void
   return CFA_OK;
 }
 
+
+// Experiment (not part of the public header): a whole run of ring-window devices mixed in ONE
+// streaming launch. Workgroups walk the (device, tile) space in order, so there is one launch
+// ramp per run instead of one per device; every device's sources are computed from the stack
+// base, the row pitch and the ring wrap-around (no pointer table). Same loads, fold and
+// write-through store as the production mix_vec_kernel<8, SEQ, 4, true>, so the output is
+// identical. For tools/probe/multi_mix.py.
+namespace {
+__global__ __launch_bounds__(kBlock) void mix8_multi_kernel(const float* models, float* outs,
+                                                            long long pitch, int L, int d0,
+                                                            unsigned tiles_per_dev, unsigned total,
+                                                            Fanin f, long long nvec) {
+  constexpr int U = 4;
+  constexpr long long kTile = (long long)kBlock * U;
+  for (unsigned t = blockIdx.x; t < total; t += gridDim.x) {
+    const unsigned rel = t / tiles_per_dev;
+    const int d = d0 + (int)rel;
+    const long long base = (long long)(t - rel * tiles_per_dev) * kTile + threadIdx.x;
+    const float* src[9];
+    src[0] = models + (long long)d * pitch;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = j < 4 ? j - 4 : j - 3;  // -4..-1, 1..4: the window order of the reference
+      src[j + 1] = models + (long long)(((d + o) % L + L) % L) * pitch;
+    }
+    f4 v[U][9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(src[k], base + (long long)u * kBlock);
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(outs + (long long)d * pitch), 0, (unsigned)(nvec * 16), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f4 y = fold<8, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
+                                             (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_multi(
+    float* outs, const float* models, size_t pitch, int L, int d0, int nd, const float* alphas,
+    size_t P, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  if (L < 9 || d0 < 0 || nd < 1 || d0 + nd > L || pitch < P) return fail(CFA_E_INVALID, "bad run");
+  Fanin f{};
+  for (int j = 0; j < 8; ++j) f.c[j + 1] = alphas[j];
+  const long long nvec = (long long)P / 4;
+  const unsigned tiles = (unsigned)(nvec / (kBlock * 4));
+  const unsigned total = tiles * (unsigned)nd;
+  const unsigned grid = (unsigned)(device_cus() * (blocks_per_cu > 0 ? blocks_per_cu : 2));
+  mix8_multi_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(models, outs, (long long)pitch, L, d0,
+                                                              tiles, total, f, nvec);
+  return check_launch("mix8_multi");
+}
