@@ -106,6 +106,7 @@ SIGNATURES = {
     "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
     "cfa_payload_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
     "cfa_payload_free": (None, [_c_void_p]),
+    "cfa_host_device_pointer": (_c_int, [_c_void_p, _PP]),
     "cfa_payload_num_keys": (_c_int, [_c_void_p]),
     "cfa_payload_key": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_size_t)]),
     "cfa_payload_info": (_c_int, [_c_void_p, ctypes.c_char_p, _c_int_p, _c_int_p, _c_int64_p, _c_int64_p]),

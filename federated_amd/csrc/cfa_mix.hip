@@ -15,6 +15,17 @@
 #include "cfa_internal.h"
 
 extern "C" int cfa_version(void) { return CFA_VERSION; }
+
+extern "C" int cfa_host_device_pointer(const void* host, void** dev) {
+  if (!host || !dev) return fail(CFA_E_INVALID, "null pointer");
+  *dev = nullptr;
+  void* p = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&p, const_cast<void*>(host), 0);
+  if (e != hipSuccess || !p)
+    return fail(CFA_E_HIP, "hipHostGetDevicePointer: %s (not pinned host memory?)", hipGetErrorString(e));
+  *dev = p;
+  return CFA_OK;
+}
 extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }
 // Used by cfa_comm.cpp so every translation unit reports through one thread-local message.
 extern "C" __attribute__((visibility("hidden"))) void cfa_internal_set_error(const char* msg) {

@@ -138,6 +138,34 @@ class Engine:
                       self.stream_handle(stream))
         return out
 
+    @staticmethod
+    def host_device_ptr(t: torch.Tensor) -> int:
+        """Device address of a pinned host tensor (cfa_host_device_pointer)."""
+        if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_pinned():
+            raise ValueError("expected a pinned host tensor (pin_memory=True)")
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("expected a contiguous fp32 tensor")
+        dev = ctypes.c_void_p()
+        _lib.call("cfa_host_device_pointer", ctypes.c_void_p(t.data_ptr()), ctypes.byref(dev))
+        return int(dev.value)
+
+    def mix_seq_pinned(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
+                       alphas: Sequence[float], stream=None) -> torch.Tensor:
+        """mix_seq on buckets that live in pinned HOST memory (f2): the kernel reads them over
+        PCIe and writes ``out`` (pinned host) directly, with no staging copies, so the link's
+        read and write directions overlap. Asynchronous on ``stream`` like mix_seq; the caller
+        synchronises before reading ``out``. Results equal mix_seq on device copies."""
+        P = local.numel()
+        for name, t in [("out", out), ("local", local)] + [(f"nbrs[{j}]", x) for j, x in enumerate(nbrs)]:
+            if t.numel() != P:
+                raise ValueError(f"{name} has {t.numel()} elements, expected {P}")
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
+        table = _lib.ptr_table([self.host_device_ptr(x) for x in nbrs])
+        _lib.call("cfa_mix_seq_f32", self.host_device_ptr(out), self.host_device_ptr(local), table,
+                  _lib.float_array(alphas), len(nbrs), P, self.stream_handle(stream))
+        return out
+
     def mix_seq_div(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
                     alphas: Sequence[float], divisors: Sequence[float], stream=None) -> torch.Tensor:
         """out = fold_j(w <- w + (alphas[j]*(nbrs[j] - w)) / divisors[j]) (FedAvg form)."""

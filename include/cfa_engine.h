@@ -360,6 +360,17 @@ CFA_API int cfa_reduce_sum_f32(void* comm, const float* send, float* recv, size_
                        void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * (f2) Host-resident buckets without staging copies. Device address of a pinned host buffer
+ * (hipHostMalloc, torch pin_memory). Passing it to the mix entry points makes the kernel read
+ * its buckets over PCIe and write the result straight into host memory: no H2D/D2H staging,
+ * and the link's two directions are busy at once. Replaces the staging copies around the mix
+ * when buckets arrive in host memory: TF1/consensus/cfa.py:108-117 (.mat loads),
+ * TF2 FL_threads_CIFAR100.py:424-428 (.npy), FL_over_MQTT/learner_consensus.py:136-145.
+ * Fails (CFA_E_HIP) for memory the runtime has not mapped for the device.
+ */
+CFA_API int cfa_host_device_pointer(const void* host, void** dev);
+
+/* ---------------------------------------------------------------------------------------
  * (f2) MQTT model payloads, host side. FL_over_MQTT ships models as
  *   pickle.dumps({'model_layer{k}': w_k.tolist(), 'device': i, 'framecount': f,
  *                 'local_epoch': e, 'training_end': b})

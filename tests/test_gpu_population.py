@@ -66,7 +66,31 @@ def test_host_staging_e2e_small(gpu):
     from federated_amd.staging import measure_e2e
     r = measure_e2e(gpu, 1_000_003, 4, reps=2, chunks=4)
     assert r["pipelined_equals_device_result"]
-    assert r["serial"]["ms"] > 0 and r["h2d_GBps"] > 0
+    assert r["zero_copy_equals_device_result"]
+    assert r["serial"]["ms"] > 0 and r["h2d_GBps"] > 0 and r["zero_copy"]["ms"] > 0
+
+
+@pytest.mark.parametrize("P,n", [(1, 1), (4099, 3), (262_147, 8)])
+def test_mix_seq_pinned_host_buckets(gpu, P, n):
+    """Zero-copy form (f2): the kernel reads pinned host buckets over PCIe and writes the pinned
+    host output; bit-exact against the oracle's sequential rule."""
+    g = torch.Generator().manual_seed(P + n)
+    local = torch.randn(P, generator=g).pin_memory()
+    nbrs = [torch.randn(P, generator=g).pin_memory() for _ in range(n)]
+    out = torch.full((P,), float("nan")).pin_memory()
+    alphas = [1.0 / (n + 1)] * n
+    gpu.mix_seq_pinned(out, local, nbrs, alphas)
+    torch.cuda.synchronize()
+    ref = sequential_mix(local.numpy(), [x.numpy() for x in nbrs], alphas)
+    assert np.array_equal(out.numpy(), ref)
+
+
+def test_mix_seq_pinned_rejects_pageable_and_device_tensors(gpu):
+    with pytest.raises(ValueError):
+        gpu.mix_seq_pinned(torch.empty(8).pin_memory(), torch.empty(8), [torch.empty(8).pin_memory()], [0.5])
+    with pytest.raises(ValueError):
+        gpu.mix_seq_pinned(torch.empty(8).pin_memory(), torch.empty(8, device="cuda"),
+                           [torch.empty(8).pin_memory()], [0.5])
 
 
 def _pop_tables(L, plan_or_lists, alphas_fn, buckets, outs):
