@@ -21,6 +21,7 @@ import numpy as np
 import scipy.io as sio
 import torch
 
+from .. import _lib
 from ..engine import BucketLayout, get_engine
 
 
@@ -71,6 +72,7 @@ def savemat_retry(path: str, data: dict) -> None:
 
 PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
+PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
 
 
 class HostMixer:
@@ -195,9 +197,15 @@ class HostMixer:
         h2d, d2h = self._aux_streams()
         comp = self._stream()
         host = self._cached("h_pipe", total, pinned=True)
-        dev = self._cached("d_pipe", total)
-        d_out = self._cached("d_out", P)
         h_out = self._cached("h_out", P, pinned=True)
+        zero_copy = PIPELINE_ZERO_COPY
+        if zero_copy:  # the kernel reads the packed chunk and writes the result in host memory
+            hbase, obase = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
+            a_arr = _lib.float_array(list(alphas))
+            d_arr = _lib.float_array(list(divisors)) if divisors is not None else None
+        else:
+            dev = self._cached("d_pipe", total)
+            d_out = self._cached("d_out", P)
         models = [local] + list(nbrs)
         flat = [[torch.from_numpy(np.ascontiguousarray(np.asarray(t)).reshape(-1)) for t in m] for m in models]
         seg = [layout.segment(k) for k in range(len(layout.sizes))]
@@ -228,19 +236,30 @@ class HostMixer:
                 base = o + j * w
                 for k, x, y, lo in pieces(a, b):
                     host[base + x - a:base + y - a].copy_(flat[j][k][x - lo:y - lo])
-            with torch.cuda.stream(h2d):
-                dev[o:o + (n + 1) * w].copy_(host[o:o + (n + 1) * w], non_blocking=True)
-            comp.wait_stream(h2d)
-            src = [dev[o + j * w:o + j * w + (b - a)] for j in range(n + 1)]
-            if divisors is not None:
-                self.engine.mix_seq_div(d_out[a:b], src[0], src[1:], list(alphas), list(divisors), stream=comp)
-            else:
-                self.engine.mix_seq(d_out[a:b], src[0], src[1:], list(alphas), stream=comp)
-            d2h.wait_stream(comp)
-            with torch.cuda.stream(d2h):
-                h_out[a:b].copy_(d_out[a:b], non_blocking=True)
+            if zero_copy:
+                table = _lib.ptr_table([hbase + 4 * (o + j * w) for j in range(1, n + 1)])
+                args = (obase + 4 * a, hbase + 4 * o, table, a_arr)
+                sh = self.engine.stream_handle(comp)
+                if divisors is not None:
+                    _lib.call("cfa_mix_seq_div_f32", *args, d_arr, n, b - a, sh)
+                else:
+                    _lib.call("cfa_mix_seq_f32", *args, n, b - a, sh)
                 ev = torch.cuda.Event()
-                ev.record(d2h)
+                ev.record(comp)
+            else:
+                with torch.cuda.stream(h2d):
+                    dev[o:o + (n + 1) * w].copy_(host[o:o + (n + 1) * w], non_blocking=True)
+                comp.wait_stream(h2d)
+                src = [dev[o + j * w:o + j * w + (b - a)] for j in range(n + 1)]
+                if divisors is not None:
+                    self.engine.mix_seq_div(d_out[a:b], src[0], src[1:], list(alphas), list(divisors), stream=comp)
+                else:
+                    self.engine.mix_seq(d_out[a:b], src[0], src[1:], list(alphas), stream=comp)
+                d2h.wait_stream(comp)
+                with torch.cuda.stream(d2h):
+                    h_out[a:b].copy_(d_out[a:b], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(d2h)
             done.append(ev)
             # host work while this chunk's H2D is in flight: fault in this chunk's output pages,
             # and unpack whatever result chunks have already landed (never block on a D2H: the

@@ -252,10 +252,13 @@ def test_population_round_window_path_equals_csr(gpu, D, P, hl, hr):
 
 
 @pytest.mark.parametrize("divide", [False, True])
-def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide):
-    """HostMixer.mix's chunked pipeline (chunk-major staging, one H2D per chunk, three streams)
-    returns the single-shot result bit for bit, across layer boundaries and ragged tails."""
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide, zero_copy):
+    """HostMixer.mix's chunked pipeline (chunk-major staging; each chunk mixed in place in pinned
+    host memory, or moved by one H2D per chunk over three streams) returns the single-shot
+    result bit for bit, across layer boundaries and ragged tails."""
     from federated_amd.consensus import _runtime as R
+    monkeypatch.setattr(R, "PIPELINE_ZERO_COPY", zero_copy)
     rng = np.random.default_rng(21)
     shapes = [(1001, 333), (333,), (517, 129), (7,)]
     local = [rng.standard_normal(s).astype(np.float32) for s in shapes]

@@ -36,6 +36,11 @@ def med(fn, n=5):
     return statistics.median(ts)
 
 
+from federated_amd.consensus import _runtime as R  # noqa: E402
+
+R.PIPELINE_ZERO_COPY = False
+t_mix_copies = med(lambda: mx.mix(local, nbrs, al))
+R.PIPELINE_ZERO_COPY = True
 t_mix = med(lambda: mx.mix(local, nbrs, al))
 lay = BucketLayout.of(local)
 pinned = torch.empty((K + 1) * P, dtype=torch.float32, pin_memory=True)
@@ -56,5 +61,6 @@ def pack_torch():
 
 
 print(json.dumps({"P": P, "K": K, "hostmixer_mix_ms": round(t_mix * 1e3, 2),
+                  "hostmixer_mix_ms_copy_pipeline": round(t_mix_copies * 1e3, 2),
                   "pack_numpy_ms": round(med(pack_numpy) * 1e3, 2), "pack_torch_ms": round(med(pack_torch) * 1e3, 2),
                   "torch_threads": torch.get_num_threads(), "bytes_packed": (K + 1) * P * 4}))
