@@ -73,6 +73,7 @@ def savemat_retry(path: str, data: dict) -> None:
 PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
 PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
+SINGLE_ZERO_COPY = True            # single-shot fp32 mixes read/write pinned staging in place (no H2D/D2H)
 
 
 class HostMixer:
@@ -131,6 +132,8 @@ class HostMixer:
         if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
             return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
         st = self._stream()
+        if SINGLE_ZERO_COPY and not tf1 and compress is None:
+            return self._mix_zero_copy(layout, local, nbrs, alphas, divisors, st), None
         with torch.cuda.stream(st):
             host = self._cached("h_in", (n + 1) * P, pinned=True)
             hv = host.numpy().reshape(n + 1, P)
@@ -170,6 +173,29 @@ class HostMixer:
             flat = h_out.numpy().copy()  # the pinned buffer is reused by the next call
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
+
+    def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st) -> List[np.ndarray]:
+        """Single-shot fp32 mix without staging copies: the buckets are packed into pinned rows
+        (pitch rounded up to 4 elements, so every row stays 16-byte aligned), the kernel reads
+        them over PCIe and writes the result into pinned host memory; one synchronisation."""
+        P, n = layout.P, len(nbrs)
+        pitch = P + (-P) % 4
+        host = self._cached("h_zc", (n + 1) * pitch, pinned=True)
+        hv = host.numpy().reshape(n + 1, pitch)
+        layout.pack(local, hv[0, :P])
+        for j, x in enumerate(nbrs):
+            layout.pack(x, hv[j + 1, :P])
+        h_out = self._cached("h_out", P, pinned=True)
+        hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
+        table = _lib.ptr_table([hb + 4 * pitch * (j + 1) for j in range(n)])
+        sh = self.engine.stream_handle(st)
+        if divisors is not None:
+            _lib.call("cfa_mix_seq_div_f32", ob, hb, table, _lib.float_array(list(alphas)),
+                      _lib.float_array(list(divisors)), n, P, sh)
+        else:
+            _lib.call("cfa_mix_seq_f32", ob, hb, table, _lib.float_array(list(alphas)), n, P, sh)
+        st.synchronize()
+        return layout.unpack(h_out.numpy().copy(), copy=False)  # the pinned buffer is reused
 
     def _aux_streams(self):
         s = getattr(self._tls, "aux", None)
