@@ -74,6 +74,7 @@ PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take 
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
 PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
 SINGLE_ZERO_COPY = True            # single-shot fp32 mixes read/write pinned staging in place (no H2D/D2H)
+TF1_ZERO_COPY = True               # TF1 fp64 mixes read/write pinned staging in place (counter stays on device)
 
 
 class HostMixer:
@@ -379,10 +380,15 @@ class HostMixer:
                     x(hv[j + 1])
                 else:
                     layout.pack(x, hv[j + 1])
-            dev = self._cached("d_in64", (n + 1) * P, torch.float64)
-            dev.copy_(host, non_blocking=True)
-            d = dev.view(n + 1, P)
-            out = self._cached("d_out64", P, torch.float64)
+            zc = TF1_ZERO_COPY
+            h_out = self._cached("h_out64", P, torch.float64, pinned=True)
+            if zc:  # the kernel reads the pinned rows and writes the pinned output in place
+                hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
+            else:
+                dev = self._cached("d_in64", (n + 1) * P, torch.float64)
+                dev.copy_(host, non_blocking=True)
+                d = dev.view(n + 1, P)
+                out = self._cached("d_out64", P, torch.float64)
             mode, cb, ce, kept = 0, 0, 0, None
             if compress is not None:
                 mode, layer = compress
@@ -393,12 +399,19 @@ class HostMixer:
                 b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
                 lo, hi = max(cb, b), min(ce, e)
                 hit = kept is not None and lo < hi
-                self.engine.mix_tf1_f64(out[b:e], d[0, b:e], [d[j, b:e] for j in range(1, n + 1)],
-                                        [float(a) for a in alphas], f32, mode if hit else 0,
-                                        lo - b if hit else 0, hi - b if hit else 0,
-                                        kept if hit else None, stream=st)
-            h_out = self._cached("h_out64", P, torch.float64, pinned=True)
-            h_out.copy_(out, non_blocking=True)
+                if zc:
+                    _lib.call("cfa_mix_tf1_f64", ob + 8 * b, hb + 8 * b,
+                              _lib.ptr_table([hb + 8 * (j * P + b) for j in range(1, n + 1)]),
+                              _lib.double_array([float(a) for a in alphas]), n, int(bool(f32)), e - b,
+                              mode if hit else 0, lo - b if hit else 0, hi - b if hit else 0,
+                              kept.data_ptr() if hit else None, self.engine.stream_handle(st))
+                else:
+                    self.engine.mix_tf1_f64(out[b:e], d[0, b:e], [d[j, b:e] for j in range(1, n + 1)],
+                                            [float(a) for a in alphas], f32, mode if hit else 0,
+                                            lo - b if hit else 0, hi - b if hit else 0,
+                                            kept if hit else None, stream=st)
+            if not zc:
+                h_out.copy_(out, non_blocking=True)
             if kept is not None:
                 h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
                 h_cnt.copy_(kept, non_blocking=True)

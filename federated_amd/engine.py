@@ -143,8 +143,8 @@ class Engine:
         """Device address of a pinned host tensor (cfa_host_device_pointer)."""
         if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_pinned():
             raise ValueError("expected a pinned host tensor (pin_memory=True)")
-        if t.dtype != torch.float32 or not t.is_contiguous():
-            raise TypeError("expected a contiguous fp32 tensor")
+        if not t.is_contiguous():
+            raise TypeError("expected a contiguous tensor")
         dev = ctypes.c_void_p()
         _lib.call("cfa_host_device_pointer", ctypes.c_void_p(t.data_ptr()), ctypes.byref(dev))
         return int(dev.value)
@@ -157,6 +157,8 @@ class Engine:
         synchronises before reading ``out``. Results equal mix_seq on device copies."""
         P = local.numel()
         for name, t in [("out", out), ("local", local)] + [(f"nbrs[{j}]", x) for j, x in enumerate(nbrs)]:
+            if t.dtype != torch.float32:
+                raise TypeError(f"{name} must be fp32 (got {t.dtype})")
             if t.numel() != P:
                 raise ValueError(f"{name} has {t.numel()} elements, expected {P}")
         if len(alphas) != len(nbrs):

@@ -56,10 +56,11 @@ def copies_only():
 
 from federated_amd.consensus import _runtime as R  # noqa: E402
 
-R.SINGLE_ZERO_COPY = False
+R.SINGLE_ZERO_COPY = R.TF1_ZERO_COPY = False
 t_copies = med(lambda: mx.mix(local, nbrs, alphas))
-R.SINGLE_ZERO_COPY = True
-res = {"P": P, "mix_tf1_us": med(lambda: mx.mix_tf1(local, nbrs, alphas)),
+t_tf1_copies = med(lambda: mx.mix_tf1(local, nbrs, alphas))
+R.SINGLE_ZERO_COPY = R.TF1_ZERO_COPY = True
+res = {"P": P, "mix_tf1_us": med(lambda: mx.mix_tf1(local, nbrs, alphas)), "mix_tf1_staged_copies_us": t_tf1_copies,
        "mix_fp32_us": med(lambda: mx.mix(local, nbrs, alphas)), "mix_fp32_staged_copies_us": t_copies,
        "kernel_plus_sync_us": med(kernel_only), "h2d_d2h_plus_sync_us": med(copies_only),
        "sync_only_us": med(torch.cuda.synchronize)}
