@@ -133,8 +133,8 @@ class HostMixer:
         if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
             return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
         st = self._stream()
-        if SINGLE_ZERO_COPY and not tf1 and compress is None:
-            return self._mix_zero_copy(layout, local, nbrs, alphas, divisors, st), None
+        if SINGLE_ZERO_COPY:
+            return self._mix_zero_copy(layout, local, nbrs, alphas, divisors, st, compress, tf1)
         with torch.cuda.stream(st):
             host = self._cached("h_in", (n + 1) * P, pinned=True)
             hv = host.numpy().reshape(n + 1, P)
@@ -175,10 +175,13 @@ class HostMixer:
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
-    def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st) -> List[np.ndarray]:
+    def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st,
+                       compress=None, tf1=False) -> Tuple[List[np.ndarray], Optional[int]]:
         """Single-shot fp32 mix without staging copies: the buckets are packed into pinned rows
         (pitch rounded up to 4 elements, so every row stays 16-byte aligned), the kernel reads
-        them over PCIe and writes the result into pinned host memory; one synchronisation."""
+        them over PCIe and writes the result into pinned host memory; one synchronisation. The
+        compression count (device atomics) stays in device memory and returns by one 8-byte
+        copy."""
         P, n = layout.P, len(nbrs)
         pitch = P + (-P) % 4
         host = self._cached("h_zc", (n + 1) * pitch, pinned=True)
@@ -190,13 +193,36 @@ class HostMixer:
         hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
         table = _lib.ptr_table([hb + 4 * pitch * (j + 1) for j in range(n)])
         sh = self.engine.stream_handle(st)
-        if divisors is not None:
+        kept = None
+        if tf1 or compress is not None:
+            mode, b, e = 0, 0, 0
+            if compress is not None:
+                mode, layer = compress
+                b, e = layout.segment(layer)
+                with torch.cuda.stream(st):
+                    kept = self._cached("d_cnt", 1, torch.int64)
+                    kept.zero_()
+            kp = kept.data_ptr() if kept is not None else None
+            if tf1:
+                _lib.call("cfa_mix_tf1_f32", ob, hb, table, _lib.double_array([float(a) for a in alphas]),
+                          n, P, int(mode), int(b), int(e), kp, sh)
+            else:
+                _lib.call("cfa_mix_seq_compress_f32", ob, hb, table, _lib.float_array(list(alphas)),
+                          n, P, int(mode), int(b), int(e), kp, sh)
+        elif divisors is not None:
             _lib.call("cfa_mix_seq_div_f32", ob, hb, table, _lib.float_array(list(alphas)),
                       _lib.float_array(list(divisors)), n, P, sh)
         else:
             _lib.call("cfa_mix_seq_f32", ob, hb, table, _lib.float_array(list(alphas)), n, P, sh)
+        kept_n = None
+        if kept is not None:
+            with torch.cuda.stream(st):
+                h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
+                h_cnt.copy_(kept, non_blocking=True)
         st.synchronize()
-        return layout.unpack(h_out.numpy().copy(), copy=False)  # the pinned buffer is reused
+        if kept is not None:
+            kept_n = int(h_cnt.numpy()[0])
+        return layout.unpack(h_out.numpy().copy(), copy=False), kept_n  # the pinned buffer is reused
 
     def _aux_streams(self):
         s = getattr(self._tls, "aux", None)

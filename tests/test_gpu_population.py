@@ -326,3 +326,30 @@ def test_ring_round_rejects_bad_layouts(gpu):
         gpu.ring_round(torch.zeros(4, 1000, device="cuda"), m, torch.zeros(4, device="cuda"), 2, 2)
     with pytest.raises(_lib.CFAError, match="overlaps"):
         gpu.ring_round(m, m, torch.zeros(4, device="cuda"), 1, 1)
+
+
+@pytest.mark.parametrize("form", ["compress", "tf1", "tf1_compress", "div"])
+def test_hostmixer_zero_copy_equals_staged(gpu, monkeypatch, form):
+    """HostMixer.mix's single-shot zero-copy path (kernel on pinned staging) equals the staged
+    path (H2D, kernel, D2H) bit for bit, counts included, for every fused form."""
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(5)
+    shapes = [(3, 3, 1, 4), (4,), (4096, 6), (6,)]
+    local = [(rng.standard_normal(s) * 1e-3).astype(np.float32) for s in shapes]
+    nbrs = [[(rng.standard_normal(s) * 1e-3).astype(np.float32) for s in shapes] for _ in range(3)]
+    al = [0.25, 0.25, 0.25]
+    kw = {}
+    if "compress" in form:
+        kw["compress"] = (2, 2)
+    if form.startswith("tf1"):
+        kw["tf1"] = True
+    if form == "div":
+        kw["divisors"] = [3.0, 3.0, 3.0]
+    mx = R.mixer()
+    monkeypatch.setattr(R, "SINGLE_ZERO_COPY", False)
+    ref, kref = mx.mix(local, nbrs, al, **kw)
+    monkeypatch.setattr(R, "SINGLE_ZERO_COPY", True)
+    got, kgot = mx.mix(local, nbrs, al, **kw)
+    assert kgot == kref
+    for a, r in zip(got, ref):
+        assert a.dtype == r.dtype and np.array_equal(a, r)
