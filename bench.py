@@ -4,10 +4,18 @@
 Metric (BASELINE.json): "device-resident GB/s, CFA reduce of K neighbour fp32 param buckets;
 1/2/4/8 GPU". Workload (BASELINE.json north_star target): 8 neighbour buckets x 25M fp32 params
 mixed into each device's local model (the TF2 sequential CFA rule, eps = 1/(K+1),
-consensus_v3.py:145,153-155). The simulated device population is sharded one shard per GPU
-(weak scaling): each rank owns ``--devices-per-gpu`` devices on a wrap-around ring window of
-K = 8 neighbours; one step = one consensus round of the shard = RCCL halo exchange of the 2x4
-boundary buckets (N > 1) overlapped with the interior mixes, then the boundary mixes.
+consensus_v3.py:145,153-155), for every device of a simulated population of D = 128 devices on
+a wrap-around ring window of K = 8 neighbours. One step = one consensus round of the whole
+population.
+
+Scaling (SURVEY §8 e: "Strong scaling, fixed population"): the population stays D = 128 for
+every N; each of the N ranks (one per GPU) owns D/N devices (``--partition devices``, the
+default): a round is the routed halo exchange of the 2x4 boundary buckets of each rank
+(federated_amd/halo.py: direct plus relayed xGMI paths, sent row by row) overlapped with the
+interior mixes, each boundary device mixing as soon as the rows it reads have landed.
+``--partition params`` splits every bucket's elements over the ranks instead (no exchange);
+``--partition hybrid --device-groups G`` combines the two. ``--devices-per-gpu L`` keeps the
+per-GPU population fixed instead (weak scaling, D = L*N).
 
 value = algorithmic bytes of all mixes on all ranks / max-over-ranks wall time, with
 algorithmic bytes = (K + 2) * P * 4 per device mix (K neighbour reads + local read + output
@@ -15,6 +23,8 @@ write). Inputs are resident in HBM when the timed region starts.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU; RANK/LOCAL_RANK/WORLD_SIZE from the environment).
+If the RCCL transport cannot be opened the run exits non-zero (``--allow-fallback`` runs on a
+torch.distributed transport instead and marks the line non-comparable).
 """
 from __future__ import annotations
 
@@ -40,9 +50,28 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--params", type=int, default=25_000_000, help="P, fp32 params per bucket")
     p.add_argument("--neighbours", type=int, default=8, help="K (even: ring window K/2 per side)")
-    p.add_argument("--devices-per-gpu", type=int, default=128,
-                   help="simulated devices per GPU (128 x 100 MB models + outputs = 26 GB of HBM)")
+    p.add_argument("--devices", type=int, default=128,
+                   help="simulated devices in the whole population (fixed for every N: strong scaling)")
+    p.add_argument("--devices-per-gpu", type=int, default=None,
+                   help="weak scaling instead: this many devices per GPU (population = N x this)")
+    p.add_argument("--partition", default="devices", choices=["devices", "params", "hybrid"],
+                   help="devices: contiguous device blocks + halo exchange (default); params: every "
+                        "rank holds a 1/N element slice of every bucket (no exchange); hybrid: "
+                        "--device-groups blocks, each split over N/groups slices")
+    p.add_argument("--device-groups", type=int, default=None)
+    p.add_argument("--no-relay", action="store_true", help="halo on the direct links only")
+    p.add_argument("--no-stages", action="store_true",
+                   help="whole halo in one exchange step (boundary devices wait for all of it)")
+    p.add_argument("--no-params-leg", action="store_true",
+                   help="N > 1: skip the second, --partition params measurement")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
+    p.add_argument("--allow-fallback", action="store_true",
+                   help="if the requested transport cannot open, fall back to torch.distributed "
+                        "(nccl, then gloo) and mark the line non-comparable instead of exiting")
+    p.add_argument("--p2p-channels", type=int, default=None,
+                   help="NCCL_NCHANNELS_PER_PEER for the RCCL communicator (default: RCCL's own)")
+    p.add_argument("--cpu-pool-seconds", type=float, default=8.0,
+                   help="bounded sample of the process-pool CPU baseline (0 = skip)")
     p.add_argument("--window-batch", type=int, default=0,
                    help="B > 0: mix B consecutive devices per cfa_mix_window_f32 pass (each window row "
                         "loaded once); 0 (default) = one streaming mix per device, the judged kernel")
@@ -92,6 +121,67 @@ def cpu_baseline(P: int, K: int, seconds: float) -> dict:
                       f"({cpu_model()}), numpy {np.__version__}, {el:.1f} s"}
 
 
+def _pool_worker(args):
+    seed, P, K, seconds, barrier, q = args
+    import numpy as np
+    from oracle.cfa_oracle import sequential_mix
+    rng = np.random.default_rng(seed)
+    local = rng.standard_normal(P, dtype=np.float32)
+    nbrs = [rng.standard_normal(P, dtype=np.float32) for _ in range(K)]
+    alphas = [1.0 / (K + 1)] * K
+    barrier.wait()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        sequential_mix(local, nbrs, alphas)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    q.put((reps, el))
+
+
+def cpu_share() -> int:
+    """CPUs this process may use: its affinity set, capped by OMP_NUM_THREADS when set (a GPU
+    box's share of a large host is given there; os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline_pool(P: int, K: int, D: int, seconds: float) -> dict:
+    """the reference's process model (one OS process per simulated device,
+    FL_CFA_CNN_tf2.py:317-319), min(D, CPU share) worker processes each running the numpy
+    restatement's sequential 8 x 25M mix concurrently for a bounded time after a common start
+    barrier. Aggregate GB/s = all workers' algorithmic bytes / the longest worker's time."""
+    import multiprocessing as mp
+    import numpy as np
+    workers = min(D, cpu_share())
+    ctx = mp.get_context("spawn")
+    barrier, q = ctx.Barrier(workers), ctx.Queue()
+    procs = [ctx.Process(target=_pool_worker, args=((20261015 + w, P, K, seconds, barrier, q),))
+             for w in range(workers)]
+    t0 = time.perf_counter()
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    wall = time.perf_counter() - t0
+    reps = sum(r for r, _ in res)
+    el = max(e for _, e in res)
+    gbs = reps * (K + 2) * P * 4 / el / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": workers, "kind": "port",
+            "sample": f"{workers} processes (one per simulated device, min(D={D}, CPU share "
+                      f"{cpu_share()}) of os.cpu_count()={os.cpu_count()}), {reps} sequential CFA mixes of "
+                      f"{K} x {P} fp32 in {el:.1f} s ({cpu_model()}), numpy {np.__version__}, "
+                      f"{wall:.1f} s wall incl. start-up"}
+
+
 def load_traffic(path: str, P: int, K: int, kernel: str = None, devices_per_launch: int = 1):
     """Per-launch HBM bytes of the timed kernel from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py), if they were taken on this exact configuration."""
@@ -106,31 +196,38 @@ def load_traffic(path: str, P: int, K: int, kernel: str = None, devices_per_laun
     return None
 
 
-def open_transport(kind, rank, world, device):
-    """The requested transport; if it cannot be opened, torch.distributed P2P over an nccl
-    (= RCCL) group, then over the gloo group (host-staged) as the last resort. The transport
-    used is reported in the JSON config."""
+class TransportError(RuntimeError):
+    pass
+
+
+def open_transport(kind, rank, world, device, allow_fallback=False):
+    """The requested transport, opened collectively: every rank takes the same decision (MIN over
+    the gloo control group), so no rank is left waiting. If it cannot be opened the bench fails
+    (TransportError on every rank) unless ``allow_fallback``: then torch.distributed P2P over an
+    nccl (= RCCL) group, then over the gloo group (host-staged). Returns (transport, comparable)."""
     import torch.distributed as dist
     from federated_amd.dist import TorchTransport, make_transport
     import torch
 
-    def agree(ok: int) -> bool:  # every rank takes the same decision (MIN over the gloo group)
+    def agree(ok: int) -> bool:
         flag = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return int(flag.item()) == 1
 
-    t, ok = None, 1
+    t, ok, err = None, 1, ""
     try:
         t = make_transport(kind, rank, world, device)
     except Exception as exc:
-        ok = 0
+        ok, err = 0, str(exc)
         print(f"[bench rank {rank}] {kind} transport failed ({exc})", file=sys.stderr)
     if agree(ok):
-        return t
+        return t, True
     if t is not None:
         t.close()
-    # torch P2P over an nccl (= RCCL) group: its communicator is created lazily, so probe it with
-    # one all-reduce before trusting it
+    if not allow_fallback:
+        raise TransportError(f"the {kind} transport could not be opened on every rank"
+                             + (f" (this rank: {err})" if err else "") + "; rerun with --allow-fallback "
+                             "to measure on a torch.distributed transport (not comparable)")
     ok, group = 1, None
     try:
         group = dist.new_group(backend="nccl")
@@ -144,14 +241,83 @@ def open_transport(kind, rank, world, device):
     if agree(ok):
         t = TorchTransport(group)
         t.name = "torch-nccl"
-        return t
+        return t, False
     t = TorchTransport()
     t.name = "torch-gloo"
-    return t
+    return t, False
+
+
+def seed_shard(shard, info, P):
+    """Synthetic models: device g's whole bucket is seeded with 20261015 + g (the same values
+    for every N and partition); a rank keeps its element slice."""
+    import torch
+    lo, hi = info["slice"]
+    gen = torch.Generator(device=shard.device)
+    full = torch.empty(P, dtype=torch.float32, device=shard.device) if (lo, hi) != (0, P) else None
+    for i in range(shard.plan.L):
+        gen.manual_seed(20261015 + shard.plan.first + i)
+        if full is None:
+            shard.models[i].normal_(generator=gen)
+        else:
+            full.normal_(generator=gen)
+            shard.models[i].copy_(full[lo:hi])
+    del full
+
+
+def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
+    """Warmup, then EXACTLY ``steps`` rounds bracketed by barrier + synchronize; returns
+    (max-over-ranks seconds, per-launch kernel durations in ms)."""
+    import torch
+    import torch.distributed as dist
+
+    compute = torch.cuda.current_stream()
+    comm = torch.cuda.Stream() if shard.plan.world > 1 else None
+    interior = shard.plan.interior()
+    if not interior:
+        timed_kernel = False
+    first_i, last_i = (interior[0], interior[-1]) if interior else (None, None)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    step_idx = [0]
+
+    # Dominant-kernel timing, live in the timed region: one HIP event pair per step around the
+    # back-to-back interior mixes on the stream they run on (no events between launches, so
+    # the measurement does not perturb the round); avg launch = batch time / launches. This
+    # includes the sub-microsecond kernel boundaries, so it is a conservative (upper) bound on
+    # the kernel duration that rocprofv3 reports.
+    def timer(i, start):
+        if start and i == first_i:
+            ev[step_idx[0]][0].record(compute)
+        elif not start and i == last_i:
+            ev[step_idx[0]][1].record(compute)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(warmup):
+        shard.round(compute, comm)
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step_idx[0] = s
+        shard.round(compute, comm, timer if timed_kernel else None)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    launches = max(1, len(shard.window_passes(interior)) if args.window_batch else len(interior))
+    durations = [a.elapsed_time(b) / launches for a, b in ev] if timed_kernel else []
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, durations, launches
 
 
 def main():
     args = parse()
+    if args.p2p_channels:
+        os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
     import torch
     import torch.distributed as dist
 
@@ -170,74 +336,68 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from federated_amd.engine import get_engine
-    from federated_amd.population import RingPopulationShard, RingShardPlan
+    from federated_amd.population import make_ring_shard
 
-    P, K, L = args.params, args.neighbours, args.devices_per_gpu
+    P, K = args.params, args.neighbours
     if K % 2:
         sys.exit("--neighbours must be even (ring window K/2 per side)")
+    weak = args.devices_per_gpu is not None
+    D = args.devices_per_gpu * world if weak else args.devices
     eng = get_engine(device)
-    plan = RingShardPlan(rank, world, L, K // 2)
-    transport = None
+
+    transport, comparable = None, True
     if world > 1:
-        transport = open_transport(args.transport, rank, world, device)
-    shard = RingPopulationShard(plan, P, torch.device("cuda", device), transport, eng,
-                                window_batch=args.window_batch)
+        try:
+            transport, comparable = open_transport(args.transport, rank, world, device, args.allow_fallback)
+        except TransportError as exc:
+            print(f"[bench rank {rank}] FATAL: {exc}", file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
 
-    gen = torch.Generator(device=shard.device)
-    for i in range(L):  # synthetic models: seeded per global device id
-        gen.manual_seed(20261015 + plan.first + i)
-        shard.models[i].normal_(generator=gen)
+    def build(partition):
+        shard, info = make_ring_shard(rank, world, D, K // 2, K // 2, P, torch.device("cuda", device), transport,
+                                      eng, partition=partition, dev_groups=args.device_groups,
+                                      relay=not args.no_relay, staged=not args.no_stages,
+                                      window_batch=args.window_batch)
+        if world > 1 and "route_digest" in info:  # every rank must run the same schedule
+            digests = [None] * world
+            dist.all_gather_object(digests, info["route_digest"])
+            if len(set(digests)) != 1:
+                print(f"[bench rank {rank}] FATAL: route plans differ across ranks", file=sys.stderr, flush=True)
+                sys.exit(4)
+        seed_shard(shard, info, P)
+        return shard, info
 
-    compute = torch.cuda.current_stream()
-    comm = torch.cuda.Stream() if world > 1 else None
-
-    # Dominant-kernel timing, live in the timed region: one HIP event pair per step around the
-    # back-to-back interior mixes on the stream they run on (no events between launches, so
-    # the measurement does not perturb the round); avg launch = batch time / launches. This
-    # includes the sub-microsecond kernel boundaries, so it is a conservative (upper) bound on
-    # the kernel duration that rocprofv3 reports.
-    interior = plan.interior()
-    first_i, last_i = interior[0], interior[-1]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    step_idx = [0]
-
-    def timer(i, start):
-        if start and i == first_i:
-            ev[step_idx[0]][0].record(compute)
-        elif not start and i == last_i:
-            ev[step_idx[0]][1].record(compute)
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    for _ in range(args.warmup):
-        shard.round(compute, comm)
-    barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step_idx[0] = s
-        shard.round(compute, comm, timer)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    launches_per_step = len(shard.window_passes(interior)) if args.window_batch else len(interior)
-    durations = [a.elapsed_time(b) / launches_per_step for a, b in ev]
-    launches_timed = launches_per_step * args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    bytes_total = world * shard.bytes_per_round * args.steps
+    shard, info = build(args.partition)
+    elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
+    bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
-    per_launch_bytes = (K + 2) * P * 4 * len(interior) // launches_per_step  # algorithmic, per launch
+    interior = shard.plan.interior()
+    per_launch_bytes = (K + 2) * shard.P * 4 * len(interior) // launches_per_step  # algorithmic, per launch
     avg_ms = sum(durations) / max(1, len(durations))
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    launches_timed = launches_per_step * args.steps
+    route = info.get("route")
+
+    legs = {}
+    if world > 1 and args.partition != "params" and not args.no_params_leg:
+        del shard
+        torch.cuda.empty_cache()
+        pshard, _ = build("params")
+        pel, _, _ = run_leg(args, pshard, world, args.steps, args.warmup, timed_kernel=False)
+        legs["params"] = {"value": round(bytes_total / pel / 1e9, 2),
+                          "ms_per_step": round(pel / args.steps * 1e3, 4),
+                          "note": "same population and steps, every rank holds a 1/N element slice of "
+                                  "every bucket (SURVEY §8 e (1)); no exchange"}
+        del pshard
 
     result = None
     if rank == 0:
+        if weak:
+            scaling = "weak"
+        else:
+            scaling = "strong"
+        kernel = "window_vec_kernel" if args.window_batch else KERNEL
         result = {
             "metric": "device-resident GB/s, CFA reduce of K neighbour fp32 param buckets; 1/2/4/8 GPU",
             "value": round(value, 2),
@@ -247,27 +407,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded torch normal fp32 buckets, resident in HBM)",
             "config": {
                 "workload": ("cfa_population_round (window passes of %d devices, rows loaded once per pass): "
                              % args.window_batch if args.window_batch else "cfa_population_round: ") +
-                            "sequential CFA mix (eps=1/(K+1)) of every device "
-                            "with K ring-window neighbours, devices sharded one shard per GPU",
+                            "sequential CFA mix (eps=1/(K+1)) of every device of a fixed population with K "
+                            "ring-window neighbours" + (", population grown with N (weak scaling)" if weak else ""),
                 "params_per_bucket": P,
                 "neighbours": K,
-                "devices_per_gpu": L,
-                "devices_total": plan.D,
+                "devices_total": D,
+                "devices_per_gpu": info["devices_per_rank"],
+                "partition": info["partition"],
+                "device_groups": info["device_groups"],
+                "param_slices": info["param_slices"],
                 "bytes_per_device_mix": (K + 2) * P * 4,
                 "window_batch": args.window_batch,
                 "transport": transport.name if transport else "none",
-                "parallelism": f"population-shard{world}",
+                "comparable": comparable,
+                "halo_route": ({k: route[k] for k in ("relay", "stages", "groups", "messages",
+                                                     "max_messages_per_rank_group")}
+                               | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
+                                  "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1)}) if route else None,
+                "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
+                "parallelism": f"population-{info['partition']}{world}",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "window_vec_kernel" if args.window_batch else KERNEL,
+                "kernel": kernel,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -276,20 +445,24 @@ def main():
                 "step_avg_launch_ms_median": round(statistics.median(durations), 5) if durations else None,
                 "step_avg_launch_ms_min": round(min(durations), 5) if durations else None,
                 "launches_timed": launches_timed,
+                "bytes_per_launch": per_launch_bytes,
                 "timing": "HIP events around each step's back-to-back interior mixes / launches",
                 "traffic": load_traffic(
                     args.traffic_json or os.path.join(ROOT, "profiles", "r01_window_pmc_traffic.json"
                                                       if args.window_batch else "r01_pmc_traffic.json"),
-                    P, K, "window_vec_kernel" if args.window_batch else KERNEL,
-                    args.window_batch or 1),
+                    shard_P(info, P), K, kernel, args.window_batch or 1),
             },
         }
+        if legs:
+            result["partitions"] = legs
     if world > 1:
         dist.barrier()
-    # CPU baseline: rank 0, N = 1 only (bounded sample).
+    # CPU baselines: rank 0, N = 1 only (bounded samples).
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(P, K, args.cpu_seconds)
+            if args.cpu_pool_seconds > 0:
+                result["cpu_baseline_pool"] = cpu_baseline_pool(P, K, D, args.cpu_pool_seconds)
         else:
             result["cpu_baseline"] = None
         if args.e2e:
@@ -300,6 +473,11 @@ def main():
         transport.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def shard_P(info, P):
+    lo, hi = info["slice"]
+    return hi - lo
 
 
 if __name__ == "__main__":

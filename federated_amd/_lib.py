@@ -102,6 +102,8 @@ SIGNATURES = {
     "cfa_comm_destroy": (_c_int, [_c_void_p]),
     "cfa_halo_exchange_f32": (_c_int, [_c_void_p, _PP, _c_int_p, _c_int, _PP, _c_int_p, _c_int,
                                        _c_size_t, _c_void_p]),
+    "cfa_p2p_group_f32": (_c_int, [_c_void_p, _PP, ctypes.POINTER(_c_size_t), _c_int_p, _c_int, _PP,
+                                   ctypes.POINTER(_c_size_t), _c_int_p, _c_int, _c_void_p]),
     "cfa_allreduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
     "cfa_payload_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
@@ -219,6 +221,13 @@ def double_array(vals) -> "ctypes.Array":
 
 def int64_array(vals) -> "ctypes.Array":
     arr = (ctypes.c_int64 * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def size_array(vals) -> "ctypes.Array":
+    arr = (ctypes.c_size_t * max(1, len(vals)))()
     for i, v in enumerate(vals):
         arr[i] = v
     return arr

@@ -100,6 +100,47 @@ extern "C" int cfa_halo_exchange_f32(void* comm, const float* const* send_bufs,
   return CFA_OK;
 }
 
+extern "C" int cfa_p2p_group_f32(void* comm, const float* const* send_bufs, const size_t* send_counts,
+                                 const int* send_peers, int nsend, float* const* recv_bufs,
+                                 const size_t* recv_counts, const int* recv_peers, int nrecv,
+                                 void* stream) {
+  if (!comm) return comm_fail(CFA_E_INVALID, "null communicator");
+  if (nsend < 0 || nrecv < 0) return comm_fail(CFA_E_INVALID, "negative transfer count");
+  if ((nsend && (!send_bufs || !send_counts || !send_peers)) ||
+      (nrecv && (!recv_bufs || !recv_counts || !recv_peers)))
+    return comm_fail(CFA_E_INVALID, "null transfer table");
+  if (nsend == 0 && nrecv == 0) return CFA_OK;
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int nranks = 0;
+  CFA_NCCL_CHECK(ncclCommCount(c, &nranks));
+  for (int i = 0; i < nsend; ++i)
+    if (send_peers[i] < 0 || send_peers[i] >= nranks || (send_counts[i] && !send_bufs[i]))
+      return comm_fail(CFA_E_INVALID, "send %d: bad peer %d or null buffer", i, send_peers[i]);
+  for (int i = 0; i < nrecv; ++i)
+    if (recv_peers[i] < 0 || recv_peers[i] >= nranks || (recv_counts[i] && !recv_bufs[i]))
+      return comm_fail(CFA_E_INVALID, "recv %d: bad peer %d or null buffer", i, recv_peers[i]);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  CFA_NCCL_CHECK(ncclGroupStart());
+  for (int i = 0; i < nsend; ++i) {
+    if (!send_counts[i]) continue;
+    ncclResult_t r = ncclSend(send_bufs[i], send_counts[i], ncclFloat32, send_peers[i], c, st);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return comm_fail(CFA_E_RCCL, "ncclSend to %d: %s", send_peers[i], ncclGetErrorString(r));
+    }
+  }
+  for (int i = 0; i < nrecv; ++i) {
+    if (!recv_counts[i]) continue;
+    ncclResult_t r = ncclRecv(recv_bufs[i], recv_counts[i], ncclFloat32, recv_peers[i], c, st);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return comm_fail(CFA_E_RCCL, "ncclRecv from %d: %s", recv_peers[i], ncclGetErrorString(r));
+    }
+  }
+  CFA_NCCL_CHECK(ncclGroupEnd());
+  return CFA_OK;
+}
+
 extern "C" int cfa_allreduce_sum_f32(void* comm, const float* send, float* recv, size_t count,
                                      void* stream) {
   if (!comm) return comm_fail(CFA_E_INVALID, "null communicator");

@@ -96,22 +96,37 @@ class RcclTransport:
         s = stream if stream is not None else torch.cuda.current_stream()
         return int(s.cuda_stream)
 
-    def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
-        """Enqueue the grouped exchange on ``stream`` (asynchronous). All buffers must have the
-        same element count; the caller orders stream dependencies."""
-        if not sends and not recvs:
-            return
-        counts = {b.numel() for b, _ in list(sends) + list(recvs)}
-        if len(counts) != 1:
-            raise ValueError("halo buffers must all have the same length")
+    def prepare(self, sends: Sequence[Transfer], recvs: Sequence[Transfer]):
+        """Bind one grouped exchange (buffers of any lengths, one message each) to its ctypes
+        tables once; returns ``run(stream)``, which enqueues it with one foreign call
+        (cfa_p2p_group_f32). The buffers must stay alive and in place."""
         for b, _ in list(sends) + list(recvs):
             if not (b.is_cuda and b.dtype == torch.float32 and b.is_contiguous()):
-                raise TypeError("halo buffers must be contiguous fp32 CUDA tensors")
+                raise TypeError("exchange buffers must be contiguous fp32 CUDA tensors")
+        # messages to ourselves pair up here, in order: their lengths must agree (a remote pair's
+        # lengths are the caller's schedule, e.g. halo.RoutePlan, checked by its digest)
+        to_self = [b.numel() for b, p in sends if p == self.rank]
+        from_self = [b.numel() for b, p in recvs if p == self.rank]
+        if to_self != from_self:
+            raise ValueError(f"self messages do not pair up: sends {to_self} vs receives {from_self}")
         L = self._lib
-        L.call("cfa_halo_exchange_f32", self.comm, L.ptr_table([b.data_ptr() for b, _ in sends]),
-               L.int_array([p for _, p in sends]), len(sends),
-               L.ptr_table([b.data_ptr() for b, _ in recvs]), L.int_array([p for _, p in recvs]),
-               len(recvs), counts.pop(), self._stream(stream))
+        args = (self.comm, L.ptr_table([b.data_ptr() for b, _ in sends]), L.size_array([b.numel() for b, _ in sends]),
+                L.int_array([p for _, p in sends]), len(sends), L.ptr_table([b.data_ptr() for b, _ in recvs]),
+                L.size_array([b.numel() for b, _ in recvs]), L.int_array([p for _, p in recvs]), len(recvs))
+        keep = (list(sends), list(recvs))
+
+        def run(stream=None):
+            L.call("cfa_p2p_group_f32", *args, self._stream(stream))
+
+        run.keep = keep
+        return run
+
+    def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
+        """Enqueue one grouped exchange on ``stream`` (asynchronous): each (buffer, peer) is one
+        message of buffer.numel() floats; the caller orders stream dependencies."""
+        if not sends and not recvs:
+            return
+        self.prepare(sends, recvs)(stream)
 
     def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
         self._lib.call("cfa_allreduce_sum_f32", self.comm, buf.data_ptr(), buf.data_ptr(), buf.numel(),

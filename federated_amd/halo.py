@@ -1,0 +1,318 @@
+"""Routed halo exchange for a population sharded over the GPUs of one fully connected xGMI node.
+
+The reference has no collective at all: a simulated device reads each neighbour's published
+model from a shared directory (TF1 ``cfa.py:119-130``, TF2 ``consensus_v3.py:82-141``). When the
+population is sharded in contiguous device blocks (SURVEY §8 e), a round's only cross-shard
+traffic is the boundary buckets each rank's devices read from the neighbouring ranks. On a ring
+window that is h buckets from each side, always to the SAME two peers, so sent directly the
+whole halo rides two of the seven xGMI links of a GPU while five idle. Under strong scaling (a
+fixed population over more GPUs) the halo stays 2h buckets per rank while the mixing work
+shrinks as 1/N, so the two links become the round's critical path.
+
+This module spreads the halo over every link:
+
+* **Routing** (``route_shares``). The demand between each ordered rank pair (a, b) is split in
+  ``units`` equal parts. Each part goes direct (link a->b) or is relayed through a third rank k
+  (links a->k, k->b). A greedy pass assigns the parts one at a time to the path whose busier link
+  ends up least loaded. It is integer arithmetic with a fixed tie-break, so every rank computes
+  the same routes without talking (and ``RoutePlan.digest`` lets the caller check that).
+* **Stages.** Transfers carry a stage index: the bench's ring plan sends the rows the most
+  boundary devices need first, so those devices can mix while later rows are still in flight.
+* **Groups.** A relayed piece needs two hops, and the second may only start once the first has
+  landed. Group g holds the direct pieces and first hops of stage g plus the second hops of
+  stage g - 1, so groups run back to back on one stream and every link stays busy. Stage s is
+  complete after group s + 1 (after group s when nothing is relayed). A relay rank keeps the
+  pieces in two staging slots, by stage parity.
+* **Messages.** Each piece is one contiguous element range, so a message is one RCCL
+  send/recv of a plain buffer slice. Within a group, every rank lists its sends to a peer in the
+  order of one global message list, and the peer lists its receives in that same order, so the
+  k-th send pairs with the k-th receive (RCCL matches point-to-point operations between a rank
+  pair in issue order).
+
+Nothing here touches a GPU: ``RoutePlan`` is pure host logic (tested on CPU, with gloo at world
+sizes up to 8); ``RoutedExchange`` binds a plan to one rank's buffers and a transport.
+"""
+from __future__ import annotations
+
+import hashlib
+from collections import defaultdict
+from dataclasses import dataclass
+from typing import Callable, Dict, Hashable, List, Optional, Sequence, Tuple
+
+ALIGN = 64  # elements: every piece starts 256-byte aligned (float4 kernels, RCCL copies)
+DIRECT = -1
+
+
+@dataclass(frozen=True)
+class Transfer:
+    """Move elements [lo, hi) of bucket ``src_key`` on rank ``src`` to the same range of bucket
+    ``dst_key`` on rank ``dst``, as part of ``stage``."""
+    stage: int
+    src: int
+    dst: int
+    src_key: Hashable
+    dst_key: Hashable
+    lo: int
+    hi: int
+
+
+@dataclass(frozen=True)
+class Message:
+    """One point-to-point send/recv of ``count`` contiguous elements."""
+    group: int
+    src: int
+    dst: int
+    src_key: Hashable
+    src_off: int
+    dst_key: Hashable
+    dst_off: int
+    count: int
+
+
+def relay_key(parity: int) -> tuple:
+    return ("relay", parity)
+
+
+def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int = 32,
+                 relay: bool = True) -> Tuple[Dict[Tuple[int, int, int], List[Tuple[int, int]]], Dict]:
+    """Split every (group, a, b) demand over the direct link and 2-hop relays.
+
+    ``demand[(g, a, b)]`` is the weight (elements) rank a sends rank b in stage position g. A
+    direct piece loads link a->b in group g; a relayed piece loads a->k in group g and k->b in
+    group g + 1. Parts are assigned one at a time, stage by stage, to the path that adds least to
+    the exchange's critical path (the sum over groups of the busiest link's load, groups running
+    back to back), then to the path whose busiest link ends up least loaded, then to fewer hops,
+    then to the lower relay rank: integer arithmetic with a fixed order, so every rank computes
+    the same routes. Returns ``shares[(g, a, b)]`` = [(path, n_units)], path = DIRECT or the
+    relay rank, direct first then relays ascending, n_units summing to ``units``; and the link
+    loads per group, ``{(g, a, b): weight}``."""
+    load: Dict[Tuple[int, int, int], int] = defaultdict(int)
+    gmax: Dict[int, int] = defaultdict(int)
+    counts = {key: defaultdict(int) for key in demand}
+    keys = sorted(k for k in demand if demand[k] > 0)
+    for g in sorted({k[0] for k in keys}):
+        stage_keys = [k for k in keys if k[0] == g]
+        for _ in range(units):
+            for key in stage_keys:
+                _, a, b = key
+                w = (demand[key] + units - 1) // units
+                best, best_cost = DIRECT, None
+                cands = [DIRECT] + ([k for k in range(world) if k != a and k != b] if relay else [])
+                for k in cands:
+                    links = [(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]
+                    delta = sum(max(0, load[l] + w - gmax[l[0]]) for l in links)
+                    cost = (delta, max(load[l] + w for l in links), len(links), k)
+                    if best_cost is None or cost < best_cost:
+                        best, best_cost = k, cost
+                for l in ([(g, a, b)] if best == DIRECT else [(g, a, best), (g + 1, best, b)]):
+                    load[l] += w
+                    gmax[l[0]] = max(gmax[l[0]], load[l])
+                counts[key][best] += 1
+    shares = {}
+    for key in demand:
+        c = counts[key]
+        order = ([DIRECT] if c.get(DIRECT) else []) + sorted(k for k in c if k != DIRECT and c[k])
+        shares[key] = [(k, c[k]) for k in order]
+    return shares, dict(load)
+
+
+def _critical(shares, demand) -> int:
+    """Sum over groups of the busiest link's weight for a set of shares."""
+    load: Dict[Tuple[int, int, int], int] = defaultdict(int)
+    for (g, a, b), parts in shares.items():
+        units = sum(n for _, n in parts) or 1
+        for k, n in parts:
+            w = demand[(g, a, b)] * n // units
+            for l in ([(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]):
+                load[l] += w
+    gmax: Dict[int, int] = defaultdict(int)
+    for (g, _, _), w in load.items():
+        gmax[g] = max(gmax[g], w)
+    return sum(gmax.values())
+
+
+def _cuts(lo: int, hi: int, units: int, align: int) -> List[int]:
+    """units + 1 aligned cut points from lo to hi (first lo, last hi)."""
+    n = hi - lo
+    pts = [lo]
+    for u in range(1, units):
+        x = lo + (n * u // units) // align * align
+        pts.append(min(max(x, pts[-1]), hi))
+    pts.append(hi)
+    return pts
+
+
+class RoutePlan:
+    """The global message schedule of one routed exchange (identical on every rank)."""
+
+    def __init__(self, world: int, transfers: Sequence[Transfer], relay: bool = True, units: int = 32,
+                 align: int = ALIGN):
+        self.world = int(world)
+        self.transfers = list(transfers)
+        self.units, self.align = int(units), int(align)
+        for t in self.transfers:
+            if not (0 <= t.src < world and 0 <= t.dst < world) or t.src == t.dst or t.hi < t.lo:
+                raise ValueError(f"bad transfer {t}")
+        self.stages = sorted({t.stage for t in self.transfers})
+        self._stage_pos = {s: i for i, s in enumerate(self.stages)}
+        demand: Dict[Tuple[int, int, int], int] = defaultdict(int)
+        for t in self.transfers:
+            demand[(self._stage_pos[t.stage], t.src, t.dst)] += t.hi - t.lo
+        self.relay = bool(relay) and world >= 3
+        self.shares, _ = route_shares(world, dict(demand), self.units, self.relay)
+        if self.relay:  # keep relays only where they shorten the critical path
+            direct, _ = route_shares(world, dict(demand), self.units, False)
+            if _critical(direct, dict(demand)) <= _critical(self.shares, dict(demand)):
+                self.relay, self.shares = False, direct
+        self.groups: List[List[Message]] = [[] for _ in range(len(self.stages) + (1 if self.relay else 0))]
+        slot_use = defaultdict(int)  # (rank, stage) -> relay elements
+        self.link_elems: Dict[Tuple[int, int], int] = defaultdict(int)
+        for t in self.transfers:
+            g = self._stage_pos[t.stage]
+            cuts = _cuts(t.lo, t.hi, self.units, self.align)
+            u = 0
+            for k, n in self.shares[(g, t.src, t.dst)]:
+                x0, x1 = cuts[u], cuts[u + n]
+                u += n
+                cnt = x1 - x0
+                if cnt <= 0:
+                    continue
+                if k == DIRECT:
+                    self.groups[g].append(Message(g, t.src, t.dst, t.src_key, x0, t.dst_key, x0, cnt))
+                    self.link_elems[(t.src, t.dst)] += cnt
+                    continue
+                off = slot_use[(k, t.stage)]
+                slot_use[(k, t.stage)] = off + -(-cnt // self.align) * self.align
+                rk = relay_key(g % 2)
+                self.groups[g].append(Message(g, t.src, k, t.src_key, x0, rk, off, cnt))
+                self.groups[g + 1].append(Message(g + 1, k, t.dst, rk, off, t.dst_key, x0, cnt))
+                self.link_elems[(t.src, k)] += cnt
+                self.link_elems[(k, t.dst)] += cnt
+        self._slot = defaultdict(int)
+        for (k, _), n in slot_use.items():
+            self._slot[k] = max(self._slot[k], n)
+        while self.groups and not self.groups[-1]:
+            self.groups.pop()
+
+    # -- queries ---------------------------------------------------------------------------
+    def slot_elems(self, rank: int) -> int:
+        """Elements of one relay staging slot on ``rank`` (two slots are needed)."""
+        return self._slot.get(rank, 0)
+
+    def done_group(self, stage: int) -> int:
+        """Index of the group after which every piece of ``stage`` has landed."""
+        g = self._stage_pos[stage]
+        return min(g + 1, len(self.groups) - 1) if self.relay else g
+
+    def stages_done_after(self, group: int) -> List[int]:
+        return [s for s in self.stages if self.done_group(s) == group]
+
+    def rank_ops(self, rank: int, group: int) -> Tuple[List[Message], List[Message]]:
+        """(sends, recvs) of ``rank`` in ``group``, each in global message order."""
+        msgs = self.groups[group]
+        return [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank]
+
+    def max_link_elems(self) -> int:
+        return max(self.link_elems.values(), default=0)
+
+    def group_link_elems(self, group: int) -> Dict[Tuple[int, int], int]:
+        load: Dict[Tuple[int, int], int] = defaultdict(int)
+        for m in self.groups[group]:
+            load[(m.src, m.dst)] += m.count
+        return dict(load)
+
+    def critical_elems(self) -> int:
+        """Sum over groups of the busiest link's elements: the exchange time in units of
+        elements per link-second when groups run back to back."""
+        return sum(max(self.group_link_elems(g).values(), default=0) for g in range(len(self.groups)))
+
+    def digest(self) -> str:
+        h = hashlib.sha1()
+        for g in self.groups:
+            for m in g:
+                h.update(repr(m).encode())
+        return h.hexdigest()
+
+    def summary(self) -> dict:
+        return {
+            "world": self.world, "relay": self.relay, "units": self.units,
+            "groups": len(self.groups), "stages": len(self.stages),
+            "messages": sum(len(g) for g in self.groups),
+            "max_messages_per_rank_group": max(
+                (len(s) + len(r) for g in range(len(self.groups)) for s, r in
+                 [self.rank_ops(x, g) for x in range(self.world)]), default=0),
+            "max_link_elems": self.max_link_elems(),
+            "critical_elems": self.critical_elems(),
+        }
+
+
+class RoutedExchange:
+    """A RoutePlan bound to one rank's buffers and a transport.
+
+    ``buffers(key)`` returns the rank's 1-D tensor for a bucket key (the element ranges of the
+    plan index into it). Relay staging is allocated here. ``run`` issues the groups in order on
+    ``stream`` and calls ``stage_done(stage)`` right after the group that completes each stage,
+    so the caller can record an event there and start that stage's boundary mixes."""
+
+    def __init__(self, plan: RoutePlan, rank: int, buffers: Callable[[Hashable], "object"], transport,
+                 device=None, dtype=None):
+        import torch
+        self.plan, self.rank, self.transport = plan, int(rank), transport
+        n = plan.slot_elems(self.rank)
+        self.relay = torch.empty((2, max(n, 1)), dtype=dtype or torch.float32, device=device)
+
+        def view(key, off, cnt):
+            buf = self.relay[key[1]] if isinstance(key, tuple) and key and key[0] == "relay" else buffers(key)
+            return buf.reshape(-1)[off:off + cnt]
+
+        self.ops = []
+        for g in range(len(plan.groups)):
+            sends, recvs = plan.rank_ops(self.rank, g)
+            s = [(view(m.src_key, m.src_off, m.count), m.dst) for m in sends]
+            r = [(view(m.dst_key, m.dst_off, m.count), m.src) for m in recvs]
+            prep = getattr(transport, "prepare", None)
+            self.ops.append(prep(s, r) if prep is not None else (s, r))
+        self.done = [plan.stages_done_after(g) for g in range(len(plan.groups))]
+
+    def run(self, stream=None, stage_done: Optional[Callable[[int], None]] = None) -> None:
+        for g, op in enumerate(self.ops):
+            if callable(op):
+                op(stream)
+            else:
+                self.transport.exchange(op[0], op[1], stream)
+            if stage_done is not None:
+                for s in self.done[g]:
+                    stage_done(s)
+
+
+def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world: int = 1,
+                   lo: int = 0, hi: Optional[int] = None, slice_bounds: Optional[Sequence[int]] = None
+                   ) -> List[Transfer]:
+    """Global transfer list of a ring-window population in contiguous device blocks.
+
+    Device block d (of ``dev_world``) sends its last ``hl`` rows to block d + 1's left halo and its
+    first ``hr`` rows to block d - 1's right halo. With ``slice_world`` > 1 (hybrid partition)
+    each block is held by ``slice_world`` ranks, rank = d * slice_world + p, each holding element
+    slice p of every bucket (``slice_bounds``), and transfers stay within a slice.
+
+    Stages: the left-halo row nearest the block (device first - 1, read by all hl left boundary
+    devices) travels in stage 0, the farthest (device first - hl, read only by device 0) in stage
+    hl - 1; likewise on the right."""
+    if dev_world < 2:
+        return []
+    out: List[Transfer] = []
+    for d in range(dev_world):
+        left, right = (d - 1) % dev_world, (d + 1) % dev_world
+        for p in range(slice_world):
+            if slice_bounds is not None:
+                a, b = slice_bounds[p], slice_bounds[p + 1]
+            else:
+                a, b = lo, (P if hi is None else hi)
+            me = d * slice_world + p
+            for q in range(hl):
+                out.append(Transfer(hl - 1 - q, left * slice_world + p, me, ("models", L - hl + q),
+                                    ("left", q), 0, b - a))
+            for q in range(hr):
+                out.append(Transfer(q, right * slice_world + p, me, ("models", q), ("right", q), 0, b - a))
+    out.sort(key=lambda t: (t.stage, t.dst, t.src, str(t.dst_key)))
+    return out

@@ -96,14 +96,59 @@ class RingShardPlan:
         return sends, recvs
 
 
+def slice_bounds(P: int, parts: int, align: int = 64) -> List[int]:
+    """Element slice bounds of a P-element bucket split in ``parts`` contiguous, ``align``-aligned
+    slices (the last takes the remainder): slice p is [b[p], b[p + 1])."""
+    units = -(-P // align)
+    base, extra = divmod(units, parts)
+    b = [0]
+    for p in range(parts):
+        b.append(min(P, b[-1] + (base + (1 if p < extra else 0)) * align))
+    b[-1] = P
+    return b
+
+
+PARTITIONS = ("devices", "params", "hybrid")
+
+
+def partition_shape(partition: str, world: int, devices: int, dev_groups: Optional[int] = None
+                    ) -> Tuple[int, int]:
+    """(device groups Gd, parameter slices Gp) with Gd * Gp = world.
+
+    - ``devices``: contiguous device blocks, one per rank (Gd = world), SURVEY §8 e "Partitioning";
+      a round exchanges the ring halo between neighbouring blocks.
+    - ``params``: every rank holds all devices but only a 1/world element slice of every bucket
+      (Gp = world), SURVEY §8 e "(1) within one bucket: elements are independent"; no exchange.
+    - ``hybrid``: ``dev_groups`` device blocks, each split over world / dev_groups element
+      slices; the halo moves between the ranks holding the same slice of neighbouring blocks."""
+    if partition == "devices":
+        gd, gp = world, 1
+    elif partition == "params":
+        gd, gp = 1, world
+    elif partition == "hybrid":
+        if not dev_groups or world % dev_groups:
+            raise ValueError("hybrid partition needs dev_groups dividing the world size")
+        gd, gp = dev_groups, world // dev_groups
+    else:
+        raise ValueError(f"unknown partition {partition!r} (one of {PARTITIONS})")
+    if devices % gd:
+        raise ValueError(f"{devices} devices do not split into {gd} equal blocks")
+    return gd, gp
+
+
 class RingPopulationShard:
     """Device-resident buckets of one shard plus its halo buffers, and the round itself."""
 
     def __init__(self, plan: RingShardPlan, P: int, device, transport=None, engine=None,
-                 dtype=torch.float32, window_batch: int = 0):
+                 dtype=torch.float32, window_batch: int = 0, route=None, rank: Optional[int] = None):
         """``window_batch`` = B > 0 mixes B consecutive devices per ``cfa_mix_window_f32`` pass,
         loading each row of their shared window once (identical results); 0 = one streaming
-        mix per device."""
+        mix per device.
+
+        ``route`` (a ``halo.RoutePlan`` over the global ranks, e.g. from ``make_ring_shard``)
+        replaces the single grouped exchange: the halo travels in stages over direct and relayed
+        paths, and each boundary device mixes as soon as the stages it reads have landed.
+        ``rank`` is this shard's global rank in that plan (default ``plan.rank``)."""
         if window_batch and not (1 <= window_batch <= 8 and plan.hl <= 4 and plan.hr <= 4):
             raise ValueError("window_batch must be 1..8 with at most 4 neighbours per side")
         self.window_batch = int(window_batch)
@@ -118,6 +163,38 @@ class RingPopulationShard:
         self.transport = transport
         self.engine = engine
         self.alphas = [1.0 / (plan.K + 1)] * plan.K
+        self.rank = plan.rank if rank is None else int(rank)
+        self.route = route
+        if route is None and plan.world > 1:
+            route = self._direct_route()
+        self._route_plan = route
+        self._routed = None
+        self._launch = {}
+        # stage after which each boundary device can mix (the latest stage of the halo rows it reads)
+        self._ready = {}
+        if route is not None:
+            stage_of = {}
+            for t in route.transfers:
+                if t.dst == self.rank:
+                    stage_of[t.dst_key] = t.stage
+            for i in self.plan.boundary():
+                g = plan.first + i
+                st = [stage_of[self.plan.locate(j)] for j in plan.neighbours(g) if self.plan.locate(j)[0] != "local"]
+                self._ready[i] = max(st) if st else -1
+
+    def _direct_route(self):
+        """One-stage, direct-only plan: the grouped exchange of round 1 (every halo bucket one
+        message on its direct link)."""
+        from .halo import RoutePlan, ring_transfers
+        p = self.plan
+        tr = [t for t in ring_transfers(p.world, p.L, p.hl, p.hr, self.P)]
+        tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
+        return RoutePlan(p.world, tr, relay=False)
+
+    def buffer(self, key) -> torch.Tensor:
+        """Row tensor of a route key: ("models", row), ("left", row) or ("right", row)."""
+        name, row = key
+        return self.models[row] if name == "models" else self.halo[name][row]
 
     def bucket(self, g: int) -> torch.Tensor:
         where, row = self.plan.locate(g)
@@ -127,16 +204,26 @@ class RingPopulationShard:
         g = self.plan.first + i
         return [self.bucket(j) for j in self.plan.neighbours(g)]
 
+    def routed(self):
+        """The RoutedExchange of this shard (built on first use: it allocates relay staging)."""
+        if self._routed is None and self._route_plan is not None:
+            from .halo import RoutedExchange
+            self._routed = RoutedExchange(self._route_plan, self.rank, self.buffer, self.transport,
+                                          self.device, self.models.dtype)
+        return self._routed
+
     def exchange(self, stream=None) -> None:
-        sends, recvs = self.plan.halo_transfers()
-        if not sends and not recvs:
-            return
-        s = [(self.models[row], peer) for row, peer in sends]
-        r = [(self.halo[name][row], peer) for (name, row), peer in recvs]
-        self.transport.exchange(s, r, stream)
+        """The whole halo exchange, issued on ``stream`` (synchronous for host transports)."""
+        r = self.routed()
+        if r is not None:
+            r.run(stream)
 
     def mix_device(self, i: int, stream=None) -> None:
-        self.engine.mix_seq(self.mixed[i], self.models[i], self.sources(i), self.alphas, stream)
+        fn = self._launch.get(i)
+        if fn is None and self.engine is not None:
+            fn = self._launch[i] = self.engine.prepare_mix_seq(self.mixed[i], self.models[i], self.sources(i),
+                                                              self.alphas)
+        fn(stream)
 
     def window_passes(self, devices: List[int]) -> List[List[int]]:
         """Runs of consecutive local devices, cut into passes of at most window_batch."""
@@ -173,22 +260,82 @@ class RingPopulationShard:
             if timer:
                 timer(i, False)
 
+    def stage_sets(self) -> List[Tuple[int, List[int]]]:
+        """[(stage, boundary devices that can mix once that stage has landed)], stage order."""
+        by = {}
+        for i, s in self._ready.items():
+            by.setdefault(s, []).append(i)
+        return [(s, sorted(by[s])) for s in sorted(by)]
+
     def round(self, compute_stream: Optional[torch.cuda.Stream] = None,
               comm_stream: Optional[torch.cuda.Stream] = None, timer=None) -> None:
-        """One consensus round: halo exchange on ``comm_stream`` overlapped with interior mixes on
-        ``compute_stream``, then the boundary mixes once the halo has landed. ``timer`` (optional)
-        is called as timer(i, start) around each interior mix to time the kernel."""
+        """One consensus round: the halo exchange on ``comm_stream`` overlapped with the interior
+        mixes on ``compute_stream``; each boundary device mixes once the stages it reads have
+        landed. ``timer`` (optional) is called as timer(i, start) around each interior mix."""
         cs = compute_stream or torch.cuda.current_stream(self.device)
-        if self.plan.world > 1:
-            ms = comm_stream or cs
-            ms.wait_stream(cs)  # models are ready (e.g. written by SGD) before they leave
-            self.exchange(ms)
+        routed = self.routed() if self.plan.world > 1 else None
+        if routed is None:
+            self._mix_set(self.plan.interior(), cs, timer)
+            self._mix_set(self.plan.boundary(), cs)
+            return
+        ms = comm_stream or cs
+        ms.wait_stream(cs)  # models are ready (e.g. written by SGD) before they leave
+        sets = self.stage_sets()
+        events = {}
+        on_gpu = ms.device.type == "cuda" if hasattr(ms, "device") else True
+
+        def landed(stage):
+            if on_gpu and ms is not cs:
+                ev = torch.cuda.Event()
+                ev.record(ms)
+                events[stage] = ev
+
+        routed.run(ms, landed)
         self._mix_set(self.plan.interior(), cs, timer)
-        if self.plan.world > 1:
-            cs.wait_stream(comm_stream or cs)
-        self._mix_set(self.plan.boundary(), cs)
+        for stage, devs in sets:
+            ev = events.get(stage)
+            if ev is not None:
+                cs.wait_event(ev)
+            elif ms is not cs:
+                cs.wait_stream(ms)
+            self._mix_set(devs, cs)
+        if ms is not cs:
+            cs.wait_stream(ms)  # the next round's exchange must not overwrite a halo still read
 
     @property
     def bytes_per_round(self) -> int:
         """Algorithmic HBM bytes of the mixes: (K + 2) * P * 4 per device."""
         return self.plan.L * (self.plan.K + 2) * self.P * self.models.element_size()
+
+
+def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: int, device,
+                    transport=None, engine=None, partition: str = "devices",
+                    dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
+                    window_batch: int = 0, dtype=torch.float32):
+    """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
+    (strong scaling: the population does not grow with ``world``).
+
+    Returns (shard, info): ``shard.P`` is this rank's slice length and ``info`` holds the
+    partition, its (Gd, Gp) shape, this rank's element slice [lo, hi) of every bucket and the
+    route summary. ``relay`` spreads the halo over relayed xGMI paths; ``staged`` sends it row by
+    row so boundary devices mix as their rows land (both only matter when Gd > 1)."""
+    from .halo import RoutePlan, ring_transfers
+    gd, gp = partition_shape(partition, world, devices, dev_groups)
+    d, p = divmod(rank, gp)
+    bounds = slice_bounds(P, gp)
+    L = devices // gd
+    plan = RingShardPlan(d, gd, L, hl, hr)
+    route = None
+    if gd > 1:
+        tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
+        if not staged:
+            tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
+        route = RoutePlan(world, tr, relay=relay)
+    shard = RingPopulationShard(plan, bounds[p + 1] - bounds[p], device, transport, engine, dtype,
+                                window_batch, route=route, rank=rank)
+    info = {"partition": partition, "device_groups": gd, "param_slices": gp,
+            "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L}
+    if route is not None:
+        info["route"] = route.summary()
+        info["route_digest"] = route.digest()
+    return shard, info

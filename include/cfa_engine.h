@@ -353,6 +353,16 @@ CFA_API int cfa_comm_destroy(void* comm);
 CFA_API int cfa_halo_exchange_f32(void* comm, const float* const* send_bufs, const int* send_peers,
                           int nsend, float* const* recv_bufs, const int* recv_peers, int nrecv,
                           size_t P, void* stream);
+/* Grouped point-to-point exchange of element ranges with per-message lengths: send_bufs[i]
+ * (send_counts[i] floats) goes to rank send_peers[i]; recv_bufs[i] (recv_counts[i] floats) is
+ * filled from recv_peers[i]. One RCCL group; messages between one rank pair pair up in issue
+ * order. This is the step of the routed (multi-link, relayed) halo exchange: a group carries
+ * the direct pieces and first relay hops of one stage and the second hops of the previous one
+ * (federated_amd/halo.py). Zero-length messages are skipped on both sides. Replaces the same
+ * file polling as cfa_halo_exchange_f32 (TF1/consensus/cfa.py:119-130). */
+CFA_API int cfa_p2p_group_f32(void* comm, const float* const* send_bufs, const size_t* send_counts,
+                      const int* send_peers, int nsend, float* const* recv_bufs,
+                      const size_t* recv_counts, const int* recv_peers, int nrecv, void* stream);
 /* Sum all-reduce / reduce of pre-scaled buckets (FedAvg / parameter-split sums). */
 CFA_API int cfa_allreduce_sum_f32(void* comm, const float* send, float* recv, size_t count,
                           void* stream);

@@ -44,6 +44,32 @@ def test_rccl_transport_world1():
         t.close()
 
 
+def test_rccl_p2p_group_world1_ragged_messages():
+    """cfa_p2p_group_f32 (the routed halo's step): several self messages of different lengths
+    and 256-byte-aligned offsets into one buffer, paired in issue order; a prepared group runs
+    twice with the same tables; zero-length messages are skipped."""
+    from federated_amd.dist import RcclTransport
+    t = RcclTransport(0, 1, 0)
+    try:
+        src = torch.randn(3 * 4096 + 123, device="cuda")
+        dst = torch.zeros_like(src)
+        cuts = [0, 4096, 4096, 2 * 4096 + 64, src.numel()]
+        sends = [(src[a:b], 0) for a, b in zip(cuts, cuts[1:])]
+        recvs = [(dst[a:b], 0) for a, b in zip(cuts, cuts[1:])]
+        run = t.prepare(sends, recvs)
+        run()
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+        src.normal_()
+        run(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+        with pytest.raises(ValueError):
+            t.prepare(sends, recvs[::-1])
+    finally:
+        t.close()
+
+
 def test_population_shard_with_rccl_transport_world1(gpu):
     """world_size 1 never exchanges; the transport object is accepted and idle."""
     from federated_amd.dist import RcclTransport
