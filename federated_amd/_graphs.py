@@ -18,6 +18,7 @@ from typing import Callable, Dict, Tuple
 import torch
 
 BLOCK_PERIODS = 8  # periods per replay of the large graph
+CAPTURE_MODE = "global"  # torch.cuda.graph capture_error_mode (hipStreamCaptureModeGlobal)
 
 
 class RoundGraphs:
@@ -46,8 +47,9 @@ class RoundGraphs:
             was_enabled = gc.isenabled()
             gc.disable()
             try:
-                # "relaxed": the libcfa launch path may query device attributes during capture
-                with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+                # strict ("global") capture: Engine construction ran cfa_device_prepare, so the
+                # libcfa launch path queries, allocates and reconfigures nothing while capturing
+                with torch.cuda.graph(g, stream=s, capture_error_mode=CAPTURE_MODE):
                     for _ in range(periods * self.period):
                         self.step()
             finally:

@@ -51,6 +51,7 @@ _PP = ctypes.POINTER(ctypes.c_void_p)  # float* const* (host table of device poi
 SIGNATURES = {
     "cfa_version": (_c_int, []),
     "cfa_last_error": (ctypes.c_char_p, []),
+    "cfa_device_prepare": (_c_int, [_c_int]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
                                     _c_void_p, _c_void_p]),
@@ -63,6 +64,8 @@ SIGNATURES = {
                                           _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
+    "cfa_mix_tf1_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,
+                                    _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int, _c_int,
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_fold_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double),

@@ -5,10 +5,12 @@
   around each neighbour). ``pause`` here sleeps ``seconds * FEDERATED_AMD_PAUSE_SCALE``
   (default 1.0 = the reference's timing; set 0 to drop the protocol sleeps).
 * ``HostMixer``: the host-array front end of the GPU engine. Per call it flattens the caller's
-  per-layer arrays into one bucket (layer order kept), copies the local and the n neighbour
-  buckets to HBM, runs ONE libcfa kernel that folds all n neighbours (plus the optional fused
-  compression epilogue), and copies the result back. There is no CPU fallback: without a GPU
-  the engine raises.
+  per-layer arrays into one pinned staging bucket per model (layer order kept) and runs ONE
+  libcfa kernel that folds all n neighbours (plus the optional fused compression epilogue).
+  By default the kernel reads the pinned rows and writes the pinned result in place over PCIe
+  (zero-copy: ``SINGLE_ZERO_COPY`` for fp32, ``TF1_ZERO_COPY`` for the fp64 TF1 buckets);
+  switched off, the buckets move by one H2D and one D2H copy instead. Large mixes take a
+  chunk pipeline. There is no CPU fallback: without a GPU the engine raises.
 """
 from __future__ import annotations
 
@@ -70,6 +72,15 @@ def savemat_retry(path: str, data: dict) -> None:
         sio.savemat(path, data)
 
 
+def _check_coefficients(n: int, alphas, divisors=None) -> None:
+    """One coefficient (and divisor) per neighbour: the C entry points read exactly n of each,
+    so a short list would be read past its end."""
+    if len(alphas) != n:
+        raise ValueError(f"one alpha per neighbour required ({len(alphas)} alphas, {n} neighbours)")
+    if divisors is not None and len(divisors) != n:
+        raise ValueError(f"one divisor per neighbour required ({len(divisors)} divisors, {n} neighbours)")
+
+
 PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
 PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
@@ -122,14 +133,18 @@ class HostMixer:
         numpy 2, and the result is that fp64 result rounded once to fp32.
 
         Host path: the local and all neighbour buckets are packed into ONE cached
-        pinned staging buffer and moved by one async H2D copy; the result (and the kept count)
-        come back by async D2H into pinned memory; one stream synchronisation per call.
+        pinned staging buffer (rows padded to 16-byte pitch). By default (``SINGLE_ZERO_COPY``)
+        the kernel reads those rows over PCIe in place and writes the result into pinned host
+        memory: no staging copies, one stream synchronisation; a compression count stays on the
+        device and returns by one 8-byte copy. With ``SINGLE_ZERO_COPY = False`` the staging
+        moves by one async H2D copy and the result by one D2H (same kernels, same results).
         Returns (fp32 arrays with the local shapes, kept count or None).
 
         Buckets above PIPELINE_MIN_BYTES of staging (without compression or the TF1 rule) take
         the chunked pipeline ``_mix_pipelined`` instead: same kernels per chunk, same results."""
         layout = BucketLayout.of(local)
         P, n = layout.P, len(nbrs)
+        _check_coefficients(n, alphas, divisors)
         if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
             return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
         st = self._stream()
@@ -392,21 +407,25 @@ class HostMixer:
         n = len(nbrs)
         if n == 0:
             raise ValueError("mix_tf1 needs at least one neighbour model")
+        _check_coefficients(n, alphas)
         layout = BucketLayout.of(local)
         P = layout.P
         flags = [np.asarray(local[k]).dtype == np.float32 and np.asarray(nbrs[0][k]).dtype == np.float32
                  for k in range(len(local))]
         st = self._stream()
+        zc = TF1_ZERO_COPY
+        # zero-copy rows keep a pitch of an even number of fp64 (16-byte aligned rows, so the
+        # kernel's vector path applies for odd P too); the staged path copies rows of exactly P
+        pitch = P + (P & 1) if zc else P
         with torch.cuda.stream(st):
-            host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
-            hv = host.numpy().reshape(n + 1, P)
-            layout.pack(local, hv[0])
+            host = self._cached("h_in64", (n + 1) * pitch, torch.float64, pinned=True)
+            hv = host.numpy().reshape(n + 1, pitch)
+            layout.pack(local, hv[0, :P])
             for j, x in enumerate(nbrs):
                 if callable(x):  # a filler writes the flat bucket itself (e.g. a payload decoder)
-                    x(hv[j + 1])
+                    x(hv[j + 1, :P])
                 else:
-                    layout.pack(x, hv[j + 1])
-            zc = TF1_ZERO_COPY
+                    layout.pack(x, hv[j + 1, :P])
             h_out = self._cached("h_out64", P, torch.float64, pinned=True)
             if zc:  # the kernel reads the pinned rows and writes the pinned output in place
                 hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
@@ -427,7 +446,7 @@ class HostMixer:
                 hit = kept is not None and lo < hi
                 if zc:
                     _lib.call("cfa_mix_tf1_f64", ob + 8 * b, hb + 8 * b,
-                              _lib.ptr_table([hb + 8 * (j * P + b) for j in range(1, n + 1)]),
+                              _lib.ptr_table([hb + 8 * (j * pitch + b) for j in range(1, n + 1)]),
                               _lib.double_array([float(a) for a in alphas]), n, int(bool(f32)), e - b,
                               mode if hit else 0, lo - b if hit else 0, hi - b if hit else 0,
                               kept.data_ptr() if hit else None, self.engine.stream_handle(st))
@@ -454,6 +473,7 @@ class HostMixer:
         staging row ``dst`` (the MQTT payload decoder does)."""
         layout = BucketLayout.of(local)
         P, n = layout.P, len(nbrs)
+        _check_coefficients(n, alphas, divisors if rule == _lib.RULE_SEQUENTIAL_DIV else None)
         st = self._stream()
         with torch.cuda.stream(st):
             host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)

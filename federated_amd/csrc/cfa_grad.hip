@@ -611,6 +611,17 @@ int plan_chunk(const void* kernel, long long fixed, long long per_sample, int B,
 
 }  // namespace
 
+// Current device: cache its LDS size and raise every gradient kernel's dynamic-LDS limit to it
+// now, so later launches (e.g. under hipGraph capture) need no attribute call.
+int grad_prepare_device() {
+  const int lim = device_lds_max();
+  if (lim <= 65536) return CFA_OK;
+  const void* kernels[] = {(const void*)grad_cnn_kernel<16, 5>, (const void*)grad_cnn_kernel<0, 0>,
+                           (const void*)grad_2nn_kernel};
+  for (const void* k : kernels) (void)raise_lds_limit(k, lim);  // refused: launches stay within 64 KiB
+  return CFA_OK;
+}
+
 namespace {
 
 // Sum of the Sp partial buckets of each evaluation, in split order (deterministic).

@@ -76,7 +76,12 @@ static const cfa_launch_t& tune() {
   return t;
 }
 
-static int device_cus() {  // per-device CU count, cached after the first query
+}  // namespace
+
+// Per-device CU count, cached after the first query. An inline function with external linkage,
+// so every translation unit shares one cache; cfa_device_prepare() fills it before any launch
+// (the launch path then only reads it, which keeps hipGraph capture free of device queries).
+inline int device_cus() {
   static int cache[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -91,6 +96,11 @@ static int device_cus() {  // per-device CU count, cached after the first query
   if (dev >= 0 && dev < 64) __atomic_store_n(&cache[dev], cus, __ATOMIC_RELAXED);
   return cus;
 }
+
+// cfa_grad.hip: per-device LDS query and kernel LDS limits, done ahead of any capture.
+int grad_prepare_device();
+
+namespace {
 
 static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
   if (tiles <= 0) return 1;

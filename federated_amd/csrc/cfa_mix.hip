@@ -26,6 +26,15 @@ extern "C" int cfa_host_device_pointer(const void* host, void** dev) {
   *dev = p;
   return CFA_OK;
 }
+extern "C" int cfa_device_prepare(int device) {
+  int prev = 0;
+  CFA_HIP_CHECK(hipGetDevice(&prev));
+  if (device != prev) CFA_HIP_CHECK(hipSetDevice(device));
+  (void)device_cus();  // fills the shared CU-count cache
+  const int rc = grad_prepare_device();
+  if (device != prev) CFA_HIP_CHECK(hipSetDevice(prev));
+  return rc;
+}
 extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }
 // Used by cfa_comm.cpp so every translation unit reports through one thread-local message.
 extern "C" __attribute__((visibility("hidden"))) void cfa_internal_set_error(const char* msg) {
@@ -472,7 +481,7 @@ extern "C" int cfa_mix_seq_compress_f32(float* out, const float* local, const fl
   if (n == 0) {
     // No neighbours: out = local, then the epilogue (TF1/consensus/cfa_ongraphs.py:218-223).
     if (out != local && P > 0)
-      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDeviceToDevice, st));
+      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDefault, st));
     return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin,
                                      kept_count, stream);
   }

@@ -397,6 +397,14 @@ static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
 extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* const* nbrs,
                                const double* alphas, int n, size_t P, int mode, size_t cbegin,
                                size_t cend, unsigned long long* kept_count, void* stream) {
+  return cfa_mix_tf1_ex_f32(out, local, nbrs, alphas, n, P, mode, cbegin, cend, kept_count, nullptr,
+                            stream);
+}
+
+extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* const* nbrs,
+                                  const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                                  size_t cend, unsigned long long* kept_count, double* scratch_in,
+                                  void* stream) {
   if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
   if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "null kept_count");
   // With a counter the epilogue runs (mode 0 keeps, and counts, every element of the range).
@@ -412,7 +420,7 @@ extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* cons
   if (n == 0) {
     // No neighbour: the bucket is the local model (fp32), then the epilogue (cfa_ongraphs.py:218-223).
     if (out != local && P > 0)
-      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDeviceToDevice, st));
+      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDefault, st));
     if (!compress) return CFA_OK;
     return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin, kept_count,
                                      stream);
@@ -429,9 +437,18 @@ extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* cons
     if (head > P) head = P;
     nvec = (P - head) / 4;
   }
-  double* scratch = nullptr;
-  if (n > CFA_MAX_FANIN)
+  double* scratch = scratch_in;
+  bool owned = false;
+  if (n > CFA_MAX_FANIN && !scratch) {
+    // no caller scratch: a stream-ordered allocation, which a hipGraph capture must not contain
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    CFA_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return fail(CFA_E_INVALID, "cfa_mix_tf1_f32: %d > %d neighbours under graph capture need a "
+                  "caller scratch bucket (cfa_mix_tf1_ex_f32)", n, CFA_MAX_FANIN);
     CFA_HIP_CHECK(hipMallocAsync((void**)&scratch, P * sizeof(double), st));
+    owned = true;
+  }
   int rc = CFA_OK;
   for (int done = 0; done < n && rc == CFA_OK;) {
     const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
@@ -440,7 +457,7 @@ extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* cons
                   nbrs + done, alphas + done, m, P, head, nvec, cp, last ? compress : 0, st);
     done += m;
   }
-  if (scratch) {
+  if (owned) {
     hipError_t e = hipFreeAsync(scratch, st);
     if (rc == CFA_OK && e != hipSuccess) return fail(CFA_E_HIP, "hipFreeAsync: %s", hipGetErrorString(e));
   }

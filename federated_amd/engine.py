@@ -104,6 +104,9 @@ class Engine:
     def __init__(self, device=None):
         self.device = _require_gpu(device)
         self.lib = _lib.load()
+        # device attributes cached and kernel LDS limits raised now, so no launch queries the
+        # device (hipGraph captures of engine launches run in the strict mode)
+        _lib.call("cfa_device_prepare", int(self.device.index))
 
     # -- helpers ---------------------------------------------------------------------------
     def stream_handle(self, stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -235,6 +238,8 @@ class Engine:
             if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 1 or x.numel() != P:
                 raise ValueError(f"nbrs[{j}] must be a 1-D fp32 CUDA view of {P} elements")
             strides.append(int(x.stride(0)))
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
         _lib.call("cfa_mix_strided_f32", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.int64_array(strides),
                   _lib.float_array(alphas), len(nbrs), P, self.stream_handle(stream))
@@ -250,6 +255,8 @@ class Engine:
         for j, x in enumerate(nbrs):
             _check_bucket(x, f"nbrs[{j}]", P)
         self._check_counter(kept)
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
         _lib.call("cfa_mix_seq_compress_f32", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.float_array(alphas),
                   len(nbrs), P, int(mode), int(cbegin), int(cend), kept.data_ptr(),
@@ -269,10 +276,19 @@ class Engine:
             _check_bucket(x, f"nbrs[{j}]", P)
         if kept is not None:
             self._check_counter(kept)
-        _lib.call("cfa_mix_tf1_f32", out.data_ptr(), local.data_ptr(),
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
+        # above CFA_MAX_FANIN the passes chain through an fp64 scratch bucket from torch's
+        # allocator (stream-ordered, and capturable), not a library allocation
+        scratch = (torch.empty(P, dtype=torch.float64, device=self.device)
+                   if len(nbrs) > _lib.CFA_MAX_FANIN else None)
+        _lib.call("cfa_mix_tf1_ex_f32", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas),
                   len(nbrs), P, int(mode), int(cbegin), int(cend),
-                  kept.data_ptr() if kept is not None else None, self.stream_handle(stream))
+                  kept.data_ptr() if kept is not None else None,
+                  scratch.data_ptr() if scratch is not None else None, self.stream_handle(stream))
+        if scratch is not None and stream is not None:
+            scratch.record_stream(stream)
         return out
 
     def mix_tf1_f64(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
@@ -287,6 +303,8 @@ class Engine:
             _check_bucket(x, f"nbrs[{j}]", P, F64)
         if kept is not None:
             self._check_counter(kept)
+        if len(alphas) != len(nbrs):
+            raise ValueError("one alpha per neighbour required")
         _lib.call("cfa_mix_tf1_f64", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas), len(nbrs),
                   int(bool(step0_f32)), P, int(mode), int(cbegin), int(cend),
@@ -302,6 +320,8 @@ class Engine:
         _check_bucket(out, "out", P, F64)
         for j, x in enumerate(nbrs):
             _check_bucket(x, f"nbrs[{j}]", P, F64)
+        if len(alphas) != len(nbrs) or (divisors is not None and len(divisors) != len(nbrs)):
+            raise ValueError("one alpha (and one divisor, when given) per neighbour required")
         _lib.call("cfa_fold_f64", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas),
                   _lib.double_array(divisors) if divisors is not None else None, len(nbrs), int(rule), P,

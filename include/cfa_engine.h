@@ -11,7 +11,8 @@
  *   - Plain pointers and sizes only. Buffers are caller-owned device pointers
  *     (hipMalloc / PyTorch-ROCm tensors). The library allocates no device memory on the hot
  *     path (scratch comes from the caller, e.g. the gradient workspace; the one exception is
- *     cfa_mix_tf1_f32 above CFA_MAX_FANIN neighbours, documented there). The host-only MQTT
+ *     cfa_mix_tf1_f32 above CFA_MAX_FANIN neighbours, documented there, whose caller-scratch
+ *     form is cfa_mix_tf1_ex_f32). The host-only MQTT
  *     payload codec allocates its parse tree in host memory (freed by cfa_payload_free).
  *   - `stream` is a hipStream_t passed as void*; NULL means the legacy default stream.
  *     Every compute call is asynchronous on that stream.
@@ -24,6 +25,28 @@
  *     device pointers (or host scalars for coefficients).
  *   - `out` may alias `local` / `W` (in-place update). Outputs must not alias any neighbour.
  *   - Any fan-in n >= 0 is accepted; n > CFA_MAX_FANIN is executed as several passes.
+ *   - hipGraph capture: call cfa_device_prepare(device) once per device before capturing. After
+ *     it, no entry point issues a device-attribute query, a kernel-attribute change or an
+ *     allocation on the launch path (cfa_mix_tf1_f32 above CFA_MAX_FANIN refuses capture and
+ *     points to cfa_mix_tf1_ex_f32), so captures run in the strict (global) mode.
+ *
+ * Where the ABI departs from the signatures sketched in SURVEY.md §8(b), and why
+ *   - cfa_mix_f32 / cfa_mix_seq_f32: (out, local, nbrs, coeff, n, P, stream) as sketched; the
+ *     sequential rule is its own entry (alphas, not closed-form coefficients) because the
+ *     reference's fp32 chain is three roundings per step, which no coefficient vector reproduces.
+ *   - cfa_compress_epilogue_f32 takes `mode` instead of (thr, rep): the four (thr, rep) pairs are
+ *     fixed by cfa_ongraphs.py:225-273 and the mode also selects the sparse vs DPCM test, which
+ *     (thr, rep) alone cannot express; a mode makes an inconsistent triple unrepresentable.
+ *   - cfa_mix_population_f32 takes device tables of bucket pointers (out_ptrs, src_ptrs) instead
+ *     of dense stacks: a population's devices live in separate buffers (ping-pong models, halo
+ *     rows, per-device allocations from callers) and a pointer table serves all of them with one
+ *     launch; a dense [D, P] stack is the special case (cfa_mix_ring_round_f32 takes one).
+ *   - cfa_comm_init(comm, rank, nranks, id, device): the communicator comes back through an out
+ *     parameter so the return value stays the status code like every other entry, and `device`
+ *     is explicit so a caller thread need not have selected the GPU beforehand.
+ *   - cfa_halo_exchange_f32 is joined by cfa_p2p_group_f32, with per-message counts, for the routed,
+ *     chunked halo; cfa_allreduce_scaled_f32 became cfa_allreduce_sum_f32 / cfa_reduce_sum_f32
+ *     because the pre-scaling is fused into the mix that produces the buffer (one pass fewer).
  */
 #ifndef CFA_ENGINE_H
 #define CFA_ENGINE_H
@@ -81,6 +104,11 @@ enum {
 
 CFA_API int cfa_version(void);
 CFA_API const char* cfa_last_error(void);
+
+/* Caches `device`'s CU count and LDS size and raises the gradient kernels' dynamic-LDS limit on
+ * it, so that later launches query nothing (required before a strict hipGraph capture). The
+ * calling thread's current device is restored. Idempotent. */
+CFA_API int cfa_device_prepare(int device);
 
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.
@@ -159,10 +187,19 @@ CFA_API int cfa_compress_epilogue_f32(float* y, const float* ref, int mode, size
  * may be NULL only when mode == CFA_COMPRESS_NONE (no epilogue, no count); otherwise the
  * number of elements of [cbegin, cend) NOT replaced is ADDED to it, as in
  * cfa_mix_seq_compress_f32 (mode 0: cend - cbegin). n > CFA_MAX_FANIN chains passes through an fp64 scratch bucket
- * (8 * P bytes, stream-ordered allocation), so the result still rounds once. */
+ * (8 * P bytes, stream-ordered allocation), so the result still rounds once. That allocation
+ * cannot be captured: under hipGraph capture with n > CFA_MAX_FANIN this entry fails
+ * (CFA_E_INVALID) and cfa_mix_tf1_ex_f32 must be used. */
 CFA_API int cfa_mix_tf1_f32(float* out, const float* local, const float* const* nbrs,
                             const double* alphas, int n, size_t P, int mode, size_t cbegin,
                             size_t cend, unsigned long long* kept_count, void* stream);
+
+/* cfa_mix_tf1_f32 with a caller-owned fp64 scratch bucket (device, >= P doubles, 8-byte
+ * aligned; used only when n > CFA_MAX_FANIN, may be NULL otherwise): no allocation at all. */
+CFA_API int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* const* nbrs,
+                               const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                               size_t cend, unsigned long long* kept_count, double* scratch,
+                               void* stream);
 
 /* (a1-a4) TF1 mix on fp64 buckets: the reference's own TF1 arithmetic, with no rounding to fp32.
  * Under numpy 2 the reference's chain is fp64 (eps * wf is an np.float64) over whatever arrays

@@ -95,3 +95,87 @@ def test_tf1_population_rounds_graph_equals_eager(gpu, pre, R):
     b.rounds(R)
     torch.cuda.synchronize()
     assert torch.equal(a.current, b.current) and torch.equal(a.previous, b.previous)
+
+
+def test_capture_survives_pending_garbage_strict_mode(gpu):
+    """Regression pin for the round-1 abort (commit 99a528c): a dead CUDAGraph and a dead
+    torch.cuda.Event sit in a reference cycle, so only the cycle collector can free them. If
+    that collection ran mid-capture, it would destroy HIP objects during the capture and abort
+    the process. RoundGraphs collects before capturing and pauses the collector while capturing.
+    The capture also runs in the strict ("global") mode: after cfa_device_prepare, the launch
+    path makes no device query."""
+    import gc
+    from federated_amd import _graphs
+    from federated_amd import topology as T
+    assert _graphs.CAPTURE_MODE == "global"
+
+    class Holder:
+        pass
+
+    def make_garbage():
+        h1, h2 = Holder(), Holder()
+        h1.other, h2.other = h2, h1
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.graph(g, stream=s):
+            torch.zeros(4, device="cuda").add_(1)
+        h1.graph, h2.event = g, torch.cuda.Event()
+        h1.event = torch.cuda.Event(enable_timing=True)
+        h1.event.record()
+
+    gc.disable()  # keep the cycle alive until the capture's own collection
+    try:
+        make_garbage()
+        assert gc.get_count()[0] > 0
+        D, P = 12, 4100
+        lists = T.kregular_v3(D, 2)
+        m0 = torch.randn(D, P, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+        got = m0.clone()
+        pr = T.PopulationRound(gpu, got)
+        pr.set_topology(lists, T.alphas_tf2)
+        pr.rounds(5)
+    finally:
+        gc.enable()
+    ref = m0.clone()
+    pe = T.PopulationRound(gpu, ref)
+    pe.set_topology(lists, T.alphas_tf2)
+    pe.rounds(5, graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+def test_tf1_mix_above_fanin_under_capture(gpu):
+    """cfa_mix_tf1_f32 with n > CFA_MAX_FANIN chains its passes through an fp64 scratch bucket:
+    the engine passes one from torch's allocator (cfa_mix_tf1_ex_f32), so the launch captures
+    in the strict mode and replays the eager result bit for bit; the library-allocating entry
+    refuses the capture instead of recording an allocation."""
+    from federated_amd import _lib
+    n, P = 19, 5003
+    g = torch.Generator(device="cuda").manual_seed(11)
+    local = torch.randn(P, device="cuda", generator=g)
+    nbrs = [torch.randn(P, device="cuda", generator=g) for _ in range(n)]
+    al = [0.5 / (n + 1)] * n
+    ref = torch.empty(P, device="cuda")
+    gpu.mix_tf1(ref, local, nbrs, al)
+    out = torch.full((P,), float("nan"), device="cuda")
+    graph, s = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(graph, stream=s):
+        gpu.mix_tf1(out, local, nbrs, al)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    graph2, s2 = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+    s2.wait_stream(torch.cuda.current_stream())
+    err = []
+    try:
+        with torch.cuda.graph(graph2, stream=s2):
+            try:
+                _lib.call("cfa_mix_tf1_f32", out.data_ptr(), local.data_ptr(),
+                          _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(al), n, P, 0, 0, 0,
+                          None, int(s2.cuda_stream))
+            except _lib.CFAError as exc:
+                err.append(str(exc))
+    finally:
+        torch.cuda.synchronize()
+    assert err and "graph capture" in err[0]

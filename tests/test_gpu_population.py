@@ -379,3 +379,80 @@ def test_hostmixer_zero_copy_equals_staged(gpu, monkeypatch, form):
     assert kgot == kref
     for a, r in zip(got, ref):
         assert a.dtype == r.dtype and np.array_equal(a, r)
+
+
+@pytest.mark.parametrize("n,P_odd", [(0, False), (17, False), (3, True), (17, True)])
+@pytest.mark.parametrize("form", ["plain", "compress", "tf1", "div"])
+def test_hostmixer_zero_copy_edges(gpu, monkeypatch, n, P_odd, form):
+    """Zero-copy vs staged equality at the edges the default test misses: no neighbour (the
+    C n == 0 branch copies host-mapped memory), n = 17 > CFA_MAX_FANIN (multi-pass with a
+    host-resident output) and an odd bucket length (padded pitch)."""
+    from federated_amd.consensus import _runtime as R
+    if form == "div" and n == 0:
+        pytest.skip("the FedAvg form always has at least one model")
+    rng = np.random.default_rng(n * 10 + P_odd)
+    shapes = [(3, 3, 1, 4), (4,), (257 if P_odd else 256, 6), (7 if P_odd else 6,)]
+    local = [(rng.standard_normal(s) * 1e-3).astype(np.float32) for s in shapes]
+    nbrs = [[(rng.standard_normal(s) * 1e-3).astype(np.float32) for s in shapes] for _ in range(n)]
+    al = [1.0 / (n + 1)] * n
+    kw = {"compress": (2, 2)} if form == "compress" else {"tf1": True} if form == "tf1" else {}
+    if form == "div":
+        kw["divisors"] = [float(j + 2) for j in range(n)]
+    mx = R.mixer()
+    monkeypatch.setattr(R, "SINGLE_ZERO_COPY", False)
+    ref, kref = mx.mix(local, nbrs, al, **kw)
+    monkeypatch.setattr(R, "SINGLE_ZERO_COPY", True)
+    got, kgot = mx.mix(local, nbrs, al, **kw)
+    assert kgot == kref
+    for a, r in zip(got, ref):
+        assert a.dtype == r.dtype and np.array_equal(a, r)
+    if n == 0 and form == "plain":
+        for a, x in zip(got, local):
+            assert np.array_equal(a, x)
+
+
+@pytest.mark.parametrize("n,P_odd,compress", [(2, False, None), (2, True, None), (3, True, (2, 2)),
+                                              (17, True, None), (1, False, (1, 2))])
+@pytest.mark.parametrize("mixed_dtypes", [False, True])
+def test_mix_tf1_zero_copy_equals_staged(gpu, monkeypatch, n, P_odd, compress, mixed_dtypes):
+    """HostMixer.mix_tf1 (fp64 buckets) with TF1_ZERO_COPY on equals the staged fp64 path bit
+    for bit, counts included: odd P (even fp64 pitch), fan-in above CFA_MAX_FANIN, compression,
+    and the mixed fp32/fp64 layer runs the reference produces after its first epoch."""
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(n + 100 * P_odd)
+    shapes = [(3, 3, 1, 4), (4,), (255 if P_odd else 256, 6), (7 if P_odd else 6,)]
+
+    def model(k):
+        dt = np.float64 if (mixed_dtypes and k % 2) else np.float32
+        return [(rng.standard_normal(s) * 1e-3).astype(dt) for s in shapes]
+
+    local = model(0)
+    nbrs = [model(j + 1) for j in range(n)]
+    al = [0.5 / (n + 1)] * n
+    mx = R.mixer()
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", False)
+    ref, kref = mx.mix_tf1(local, nbrs, al, compress=compress)
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", True)
+    got, kgot = mx.mix_tf1(local, nbrs, al, compress=compress)
+    assert kgot == kref
+    for a, r in zip(got, ref):
+        assert a.dtype == r.dtype and np.array_equal(a, r)
+
+
+def test_hostmixer_rejects_short_coefficient_lists(gpu, monkeypatch):
+    """the zero-copy path calls the C entries directly, which read exactly n
+    coefficients; a short alphas or divisors list must raise before any call."""
+    from federated_amd.consensus import _runtime as R
+    monkeypatch.setattr(R, "SINGLE_ZERO_COPY", True)
+    shapes = [(8, 4), (4,)]
+    local = [np.ones(s, np.float32) for s in shapes]
+    nbrs = [[np.ones(s, np.float32) for s in shapes] for _ in range(3)]
+    mx = R.mixer()
+    with pytest.raises(ValueError, match="alpha"):
+        mx.mix(local, nbrs, [0.25, 0.25])
+    with pytest.raises(ValueError, match="divisor"):
+        mx.mix(local, nbrs, [0.25] * 3, divisors=[3.0])
+    with pytest.raises(ValueError, match="alpha"):
+        mx.mix_tf1(local, nbrs, [0.25])
+    with pytest.raises(ValueError, match="alpha"):
+        mx.mix(local, nbrs, [0.25], tf1=True)
