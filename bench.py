@@ -380,16 +380,26 @@ def main():
     route = info.get("route")
 
     legs = {}
-    if world > 1 and args.partition != "params" and not args.no_params_leg:
+    if world > 1 and args.partition == "devices" and not args.no_params_leg:
         del shard
         torch.cuda.empty_cache()
-        pshard, _ = build("params")
-        pel, _, _ = run_leg(args, pshard, world, args.steps, args.warmup, timed_kernel=False)
-        legs["params"] = {"value": round(bytes_total / pel / 1e9, 2),
-                          "ms_per_step": round(pel / args.steps * 1e3, 4),
-                          "note": "same population and steps, every rank holds a 1/N element slice of "
-                                  "every bucket (SURVEY §8 e (1)); no exchange"}
-        del pshard
+        extra = [("params", None, "same population and steps, every rank holds a 1/N element slice of "
+                                  "every bucket (SURVEY §8 e (1)); no exchange")]
+        if world >= 4 and D % 2 == 0:
+            extra.append(("hybrid", 2, "same population and steps, 2 device blocks, each split over N/2 "
+                                       "element slices; routed halo between ranks holding the same slice"))
+        for part, groups, note in extra:
+            saved, args.device_groups = args.device_groups, groups
+            xshard, xinfo = build(part)
+            args.device_groups = saved
+            xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
+            leg = {"value": round(bytes_total / xel / 1e9, 2), "ms_per_step": round(xel / args.steps * 1e3, 4),
+                   "note": note}
+            if xinfo.get("route"):
+                leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
+            legs[part if groups is None else f"{part}{groups}"] = leg
+            del xshard
+            torch.cuda.empty_cache()
 
     result = None
     if rank == 0:

@@ -58,8 +58,6 @@ SIGNATURES = {
     "cfa_mix_seq_div_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_float_p, _c_int,
                                      _c_size_t, _c_void_p]),
     "cfa_mix_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
-    "cfa_mix_strided_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_int64_p, _c_float_p, _c_int,
-                                     _c_size_t, _c_void_p]),
     "cfa_mix_seq_compress_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
                                           _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,

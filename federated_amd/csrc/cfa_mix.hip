@@ -1,6 +1,6 @@
 // cfa_mix.hip — the streaming mix kernels (fp32 buckets) and their C-ABI: the sequential CFA rule,
-// the FedAvg divisor form, the linear closed form, strided gradient slices, the fused and
-// standalone compression epilogue.
+// the FedAvg divisor form, the linear closed form, the fused and standalone compression
+// epilogue.
 //
 // The reference computes the mixing step as numpy AXPY chains over whole tensors, one
 // neighbour at a time, with a file round trip between neighbours:
@@ -121,10 +121,9 @@ __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fa
   block_add_count(kept, cp.kept);
 }
 
-// Scalar path: unaligned buckets, the <4-element tail, and strided neighbours.
+// Scalar path: unaligned buckets and the <4-element tail.
 struct ScalarFanin {
   const float* src[CFA_MAX_FANIN + 1];
-  long long stride[CFA_MAX_FANIN + 1];
   float c[CFA_MAX_FANIN + 1];
   float d[CFA_MAX_FANIN + 1];
   int n;
@@ -135,19 +134,19 @@ __global__ __launch_bounds__(kBlock) void mix_scalar_kernel(float* out, ScalarFa
   unsigned kept = 0;
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P;
        i += (long long)gridDim.x * kBlock) {
-    const float w0 = f.src[0][i * f.stride[0]];
+    const float w0 = f.src[0][i];
     float w;
     if (rule == CFA_RULE_SEQUENTIAL || rule == CFA_RULE_SEQUENTIAL_DIV) {
       w = w0;
       for (int j = 1; j <= f.n; ++j) {
-        float t = f.src[j][i * f.stride[j]] - w;
+        float t = f.src[j][i] - w;
         t = f.c[j] * t;
         if (rule == CFA_RULE_SEQUENTIAL_DIV) t = t / f.d[j];
         w = w + t;
       }
     } else {
       w = f.c[0] * w0;
-      for (int j = 1; j <= f.n; ++j) w = fmaf(f.c[j], f.src[j][i * f.stride[j]], w);
+      for (int j = 1; j <= f.n; ++j) w = fmaf(f.c[j], f.src[j][i], w);
     }
     if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one(w, w0, cp, kept);
     out[i] = w;
@@ -311,10 +310,8 @@ static int mix_pass(float* out, const float* local, const float* const* nbrs, co
     if (e <= b) continue;
     ScalarFanin sf{};
     sf.src[0] = local + b;
-    sf.stride[0] = 1;
     for (int j = 0; j < n; ++j) {
       sf.src[j + 1] = nbrs[j] + b;
-      sf.stride[j + 1] = 1;
     }
     for (int k = 0; k <= n; ++k) sf.c[k] = c[k];
     for (int k = 0; k <= n; ++k) sf.d[k] = div ? div[k] : 1.0f;
@@ -422,43 +419,6 @@ extern "C" int cfa_mix_f32(float* out, const float* local, const float* const* n
     c[0] = done == 0 ? coeff[0] : 1.0f;
     for (int j = 0; j < m; ++j) c[j + 1] = coeff[done + j + 1];
     if (int rc = mix_pass(out, w, nbrs + done, c, m, P, CFA_RULE_LINEAR, nullptr, st)) return rc;
-    done += m;
-    w = out;
-  } while (done < n);
-  return CFA_OK;
-}
-
-extern "C" int cfa_mix_strided_f32(float* out, const float* local, const float* const* nbrs,
-                                   const int64_t* nbr_stride, const float* alphas, int n, size_t P,
-                                   void* stream) {
-  if (n > 0 && (!alphas || !nbr_stride)) return fail(CFA_E_INVALID, "null alphas/strides");
-  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
-  if (P == 0) return CFA_OK;
-  bool unit = true;
-  for (int j = 0; j < n; ++j) {
-    if (nbr_stride[j] < 1) return fail(CFA_E_INVALID, "stride %lld < 1", (long long)nbr_stride[j]);
-    unit = unit && nbr_stride[j] == 1;
-  }
-  if (unit) return cfa_mix_seq_f32(out, local, nbrs, alphas, n, P, stream);
-  hipStream_t st = (hipStream_t)stream;
-  int done = 0;
-  const float* w = local;
-  do {
-    const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
-    ScalarFanin sf{};
-    sf.src[0] = w;
-    sf.stride[0] = 1;
-    sf.c[0] = 1.0f;
-    for (int j = 0; j < m; ++j) {
-      sf.src[j + 1] = nbrs[done + j];
-      sf.stride[j + 1] = nbr_stride[done + j];
-      sf.c[j + 1] = alphas[done + j];
-    }
-    sf.n = m;
-    CompressParams none{};
-    mix_scalar_kernel<<<grid_for(((long long)P + kBlock - 1) / kBlock), kBlock, 0, st>>>(
-        out, sf, (long long)P, CFA_RULE_SEQUENTIAL, 0, none);
-    if (int rc = check_launch("mix_strided")) return rc;
     done += m;
     w = out;
   } while (done < n);

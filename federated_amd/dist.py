@@ -57,8 +57,26 @@ class TorchTransport:
             if dst is not src:
                 dst.copy_(src)
 
+    def _collective(self, buf: torch.Tensor, stream, fn) -> None:
+        """Run ``fn(tensor)`` on ``buf``; gloo moves host tensors only, so a device buffer is
+        staged through host memory (synchronously)."""
+        if dist.get_backend(self.group) == "gloo" and buf.is_cuda:
+            if stream is not None:
+                stream.synchronize()
+            host = buf.cpu()
+            fn(host)
+            buf.copy_(host)
+            return
+        ctx = torch.cuda.stream(stream) if (stream is not None and buf.is_cuda) else contextlib.nullcontext()
+        with ctx:
+            fn(buf)
+
     def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+        self._collective(buf, stream, lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group))
+
+    def reduce_sum(self, buf: torch.Tensor, root: int, stream=None) -> None:
+        """Sum of every rank's ``buf`` into ``buf`` on ``root`` (other ranks' buffers undefined)."""
+        self._collective(buf, stream, lambda t: dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, group=self.group))
 
     def close(self) -> None:
         pass
@@ -129,8 +147,21 @@ class RcclTransport:
         self.prepare(sends, recvs)(stream)
 
     def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
+        """In-place sum all-reduce of a contiguous fp32 device buffer, enqueued on ``stream``."""
+        self._check_collective(buf)
         self._lib.call("cfa_allreduce_sum_f32", self.comm, buf.data_ptr(), buf.data_ptr(), buf.numel(),
                        self._stream(stream))
+
+    def reduce_sum(self, buf: torch.Tensor, root: int, stream=None) -> None:
+        """In-place sum reduce to ``root``, enqueued on ``stream``."""
+        self._check_collective(buf)
+        self._lib.call("cfa_reduce_sum_f32", self.comm, buf.data_ptr(), buf.data_ptr(), buf.numel(), int(root),
+                       self._stream(stream))
+
+    @staticmethod
+    def _check_collective(buf: torch.Tensor) -> None:
+        if not (buf.is_cuda and buf.dtype == torch.float32 and buf.is_contiguous()):
+            raise TypeError("collective buffers must be contiguous fp32 CUDA tensors")
 
     def close(self) -> None:
         if self.comm:

@@ -228,23 +228,6 @@ class Engine:
                   len(nbrs), P, self.stream_handle(stream))
         return out
 
-    def mix_strided(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],
-                    alphas: Sequence[float], stream=None) -> torch.Tensor:
-        """Sequential mix where neighbour j may be a 1-D strided view (e.g. g[..., ii])."""
-        P = _check_bucket(local, "local")
-        _check_bucket(out, "out", P)
-        strides = []
-        for j, x in enumerate(nbrs):
-            if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 1 or x.numel() != P:
-                raise ValueError(f"nbrs[{j}] must be a 1-D fp32 CUDA view of {P} elements")
-            strides.append(int(x.stride(0)))
-        if len(alphas) != len(nbrs):
-            raise ValueError("one alpha per neighbour required")
-        _lib.call("cfa_mix_strided_f32", out.data_ptr(), local.data_ptr(),
-                  _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.int64_array(strides),
-                  _lib.float_array(alphas), len(nbrs), P, self.stream_handle(stream))
-        return out
-
     def mix_seq_compress(self, out: torch.Tensor, local: torch.Tensor,
                          nbrs: Sequence[torch.Tensor], alphas: Sequence[float], mode: int,
                          cbegin: int, cend: int, kept: torch.Tensor, stream=None) -> torch.Tensor:

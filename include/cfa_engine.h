@@ -44,6 +44,12 @@
  *   - cfa_comm_init(comm, rank, nranks, id, device): the communicator comes back through an out
  *     parameter so the return value stays the status code like every other entry, and `device`
  *     is explicit so a caller thread need not have selected the GPU beforehand.
+ *   - cfa_mix_strided_f32 (sketched for the `[..., devices]` gradient slices of CFA-GE,
+ *     cfa_ge_2stage.py:594-606) is not provided. Those slices arrive in host memory (loadmat),
+ *     and the host mixer gathers slot `ii` while packing the pinned staging rows, so every GPU
+ *     read is a coalesced row. Read on the device, a stride-D slice pulls a whole line per 4
+ *     useful bytes: the round-1 entry ran at 0.31 of peak with 2.5x over-fetch, so it was
+ *     retired in round 2 instead of being exposed.
  *   - cfa_halo_exchange_f32 is joined by cfa_p2p_group_f32, with per-message counts, for the routed,
  *     chunked halo; cfa_allreduce_scaled_f32 became cfa_allreduce_sum_f32 / cfa_reduce_sum_f32
  *     because the pre-scaling is fused into the mix that produces the buffer (one pass fewer).
@@ -152,13 +158,6 @@ CFA_API int cfa_mix_seq_div_f32(float* out, const float* local, const float* con
  * (TF2 parameter_server_v2.py:159-161, PS_server.py:127-134). */
 CFA_API int cfa_mix_f32(float* out, const float* local, const float* const* nbrs,
                 const float* coeff, int n, size_t P, void* stream);
-
-/* Sequential mix with element-strided neighbour buckets: element i of neighbour j is read at
- * nbrs[j][i * nbr_stride[j]]. Serves the `[..., devices]` gradient slices of CFA-GE
- * (TF1/consensus/cfa_ge_2stage.py:594-606, slice `[..., ii]`, stride = devices). */
-CFA_API int cfa_mix_strided_f32(float* out, const float* local, const float* const* nbrs,
-                        const int64_t* nbr_stride, const float* alphas, int n, size_t P,
-                        void* stream);
 
 /* Sequential mix fused with the compression epilogue of cfa_ongraphs.py:225-273.
  * The epilogue applies to elements [cbegin, cend) of the bucket (the W2 tensor), with

@@ -23,7 +23,7 @@ def header_symbols():
 
 def test_header_declares_full_abi():
     syms = header_symbols()
-    for required in ("cfa_mix_seq_f32", "cfa_mix_f32", "cfa_mix_strided_f32", "cfa_mewma_update_f32",
+    for required in ("cfa_mix_seq_f32", "cfa_mix_f32", "cfa_mewma_update_f32",
                      "cfa_compress_epilogue_f32", "cfa_mix_population_f32", "cfa_comm_init",
                      "cfa_halo_exchange_f32", "cfa_allreduce_sum_f32", "cfa_last_error", "cfa_version"):
         assert required in syms

@@ -83,20 +83,6 @@ def test_mix_linear_closed_form(gpu, n):
     assert normwise_close(out.cpu().numpy(), ref)
 
 
-def test_mix_strided_gradient_slices(gpu):
-    """[..., devices] gradient layout (cfa_ge_2stage.py:594-606): slot ii read with stride D."""
-    rng = np.random.default_rng(5)
-    P, D, ii = 50_000, 16, 7
-    local = _rand(rng, 1, P)[0]
-    stacks = [rng.standard_normal((P, D)).astype(np.float32) for _ in range(3)]
-    alphas = [0.25, 0.5, 0.125]
-    ref = O.sequential_mix(local, [s[:, ii].copy() for s in stacks], alphas)
-    dstacks = [_dev(s) for s in stacks]
-    out = torch.empty(P, dtype=torch.float32, device="cuda")
-    gpu.mix_strided(out, _dev(local), [s[:, ii] for s in dstacks], alphas)
-    assert np.array_equal(out.cpu().numpy(), ref)
-
-
 def _compress_expect(local, nbrs, alphas, mode, cb, ce):
     """fp32 chain, then the epilogue as numpy 2 evaluates it on fp32 arrays (threshold and
     replacement cast to fp32; W2 is [4096, 6])."""

@@ -456,3 +456,37 @@ def test_hostmixer_rejects_short_coefficient_lists(gpu, monkeypatch):
         mx.mix_tf1(local, nbrs, [0.25])
     with pytest.raises(ValueError, match="alpha"):
         mx.mix(local, nbrs, [0.25], tf1=True)
+
+
+@pytest.mark.parametrize("D,P,u,subset", [(8, 1_071_748, 1.0, False), (32, 24_622, 0.99, True),
+                                          (20, 4_000_003, 1.0, False)])
+def test_sharded_fedavg_world1_gpu(gpu, D, P, u, subset):
+    """ShardedFedAvg on one GPU: the closed-form pre-scaled sum (cfa_mix_f32, all D models in
+    one launch chain) equals the reference's sequential FedAvg fold (oracle.ps_fedavg,
+    parameter_server_v2.py:159-161) within 1e-5 normwise; world 1 needs no collective."""
+    from federated_amd.ps_shard import ShardedFedAvg
+    from oracle.cfa_oracle import ps_fedavg
+    g = torch.Generator(device="cuda").manual_seed(D + P)
+    ps = ShardedFedAvg(0, 1, D, P, "cuda", None, gpu, update_factor=u)
+    ps.models.normal_(generator=g)
+    ps.params.normal_(generator=g)
+    models, params = ps.models.cpu().numpy(), ps.params.cpu().numpy()
+    active = [d for d in range(D) if d % 4 != 2] if subset else list(range(D))
+    out = ps.aggregate(active).cpu().numpy()
+    ref = ps_fedavg([params], [[models[d]] for d in active], u)[0]
+    assert np.max(np.abs(out - ref)) <= 1e-5 * np.max(np.abs(ref))
+
+
+def test_rccl_reduce_sum_world1(gpu):
+    """cfa_reduce_sum_f32 through RcclTransport.reduce_sum at world size 1 (identity on root 0)."""
+    from federated_amd.dist import RcclTransport
+    t = RcclTransport(0, 1, torch.cuda.current_device())
+    try:
+        x = torch.randn(1 << 20, device="cuda")
+        ref = x.clone()
+        t.reduce_sum(x, 0)
+        t.allreduce_sum(x)
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref)
+    finally:
+        t.close()

@@ -4,7 +4,6 @@
 Each entry point runs back to back on HBM-resident buckets (HIP events around `--reps`
 launches after warm-up). Its algorithmic bytes per launch are the DESIGN.md §3 formula, so
 achieved GB/s = bytes / average launch time, and frac = that over the 8 TB/s HBM3E spec peak.
-The strided mix also reports its over-fetch: a stride-s read touches a 64-B segment per element.
 Prints one JSON line per kernel. Usage: python tools/kernel_rooflines.py [--params 25000000]
 """
 import argparse
@@ -72,17 +71,10 @@ def main():
         timed(lambda: eng.mix_seq_compress(out, local, nb[:3], al[:3], 2, 0, P, kept), R))
     rec("standalone compression epilogue (mode 2)", "cfa_compress_epilogue_f32", 3 * P * 4,
         timed(lambda: eng.compress(out, local, 2, kept), R))
-    # strided gradient slices: [P, 4] layout, slot 1 (cfa_ge_2stage.py:594-606)
-    stack = torch.randn(P // 4, 4, device="cuda", generator=g)
-    sl = stack[:, 1]
-    l4, o4 = f32()[: P // 4].contiguous(), torch.empty(P // 4, device="cuda")
-    rec("strided slices (stride 4), n=2", "cfa_mix_strided_f32", 4 * (P // 4) * 4,
-        timed(lambda: eng.mix_strided(o4, l4, [sl, sl], [0.5, 0.5]), R),
-        "each strided element read fetches a full line: HBM traffic ~4x the algorithmic neighbour bytes")
     W, s2, g2 = f32(), [f32() for _ in range(2)], [f32() for _ in range(2)]
     rec("MEWMA update, n=2", "cfa_mewma_update_f32", (3 * 2 + 2) * P * 4,
         timed(lambda: eng.mewma(W, s2, g2, 0.99, 0.1, 0.1, P // 2, False, True), R))
-    del nb, s2, g2, stack
+    del nb, s2, g2
     torch.cuda.empty_cache()
     n64 = 4
     l64, o64 = f64(), torch.empty(P, device="cuda", dtype=torch.float64)
