@@ -52,6 +52,8 @@ SIGNATURES = {
     "cfa_version": (_c_int, []),
     "cfa_last_error": (ctypes.c_char_p, []),
     "cfa_device_prepare": (_c_int, [_c_int]),
+    "cfa_stream_synchronize": (_c_int, [_c_void_p]),
+    "cfa_counter_fetch": (_c_int, [_c_void_p, _c_void_p, _c_void_p]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,
                                     _c_void_p, _c_void_p]),
@@ -195,6 +197,13 @@ def call(name: str, *args) -> None:
     rc = getattr(lib, name)(*args)
     if rc != CFA_OK:
         msg = lib.cfa_last_error()
+        raise CFAError(name, rc, msg.decode() if msg else "")
+
+
+def check(name: str, rc: int) -> None:
+    """Raise CFAError for a non-zero status returned by a direct (pre-bound) entry-point call."""
+    if rc != CFA_OK:
+        msg = load().cfa_last_error()
         raise CFAError(name, rc, msg.decode() if msg else "")
 
 

@@ -81,6 +81,21 @@ def _check_coefficients(n: int, alphas, divisors=None) -> None:
         raise ValueError(f"one divisor per neighbour required ({len(divisors)} divisors, {n} neighbours)")
 
 
+_layouts: dict = {}
+
+
+def _layout_of(arrays) -> BucketLayout:
+    """BucketLayout of the arrays' shapes, cached per shape tuple (building one costs tens of
+    microseconds of numpy calls, which a per-call drop-in path cannot afford)."""
+    key = tuple(np.shape(a) for a in arrays)
+    lay = _layouts.get(key)
+    if lay is None:
+        if len(_layouts) >= 64:
+            _layouts.clear()
+        lay = _layouts[key] = BucketLayout(key)
+    return lay
+
+
 PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
 PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
@@ -142,7 +157,7 @@ class HostMixer:
 
         Buckets above PIPELINE_MIN_BYTES of staging (without compression or the TF1 rule) take
         the chunked pipeline ``_mix_pipelined`` instead: same kernels per chunk, same results."""
-        layout = BucketLayout.of(local)
+        layout = _layout_of(local)
         P, n = layout.P, len(nbrs)
         _check_coefficients(n, alphas, divisors)
         if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
@@ -190,54 +205,64 @@ class HostMixer:
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
+    def _zc_plan(self, kind: str, layout_key: tuple, n: int, dtype) -> "_ZeroCopyPlan":
+        """Per-thread cached zero-copy plan for one (kind, layer shapes, fan-in): the layout,
+        pinned rows and output, their device addresses and the ctypes tables, built once."""
+        plans = getattr(self._tls, "plans", None)
+        if plans is None:
+            plans = self._tls.plans = {}
+        key = (kind, layout_key, n)
+        plan = plans.get(key)
+        if plan is None:
+            if len(plans) >= 16:  # bounded: drop the oldest layout
+                plans.pop(next(iter(plans)))
+            plan = plans[key] = _ZeroCopyPlan(self, layout_key, n, dtype)
+        return plan
+
     def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st,
                        compress=None, tf1=False) -> Tuple[List[np.ndarray], Optional[int]]:
         """Single-shot fp32 mix without staging copies: the buckets are packed into pinned rows
         (pitch rounded up to 4 elements, so every row stays 16-byte aligned), the kernel reads
         them over PCIe and writes the result into pinned host memory; one synchronisation. The
         compression count (device atomics) stays in device memory and returns by one 8-byte
-        copy."""
-        P, n = layout.P, len(nbrs)
-        pitch = P + (-P) % 4
-        host = self._cached("h_zc", (n + 1) * pitch, pinned=True)
-        hv = host.numpy().reshape(n + 1, pitch)
-        layout.pack(local, hv[0, :P])
-        for j, x in enumerate(nbrs):
-            layout.pack(x, hv[j + 1, :P])
-        h_out = self._cached("h_out", P, pinned=True)
-        hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
-        table = _lib.ptr_table([hb + 4 * pitch * (j + 1) for j in range(n)])
-        sh = self.engine.stream_handle(st)
-        kept = None
+        copy (cfa_counter_fetch, which also re-zeroes it). Everything but the pack, the launch
+        and the unpack is prepared once per layout (``_ZeroCopyPlan``)."""
+        n = len(nbrs)
+        plan = self._zc_plan("f32", tuple(layout.shapes), n, np.float32)
+        plan.pack(local, nbrs)
+        sh = plan.stream_handle(st)
+        lib = plan.lib
         if tf1 or compress is not None:
             mode, b, e = 0, 0, 0
             if compress is not None:
                 mode, layer = compress
                 b, e = layout.segment(layer)
-                with torch.cuda.stream(st):
-                    kept = self._cached("d_cnt", 1, torch.int64)
-                    kept.zero_()
-            kp = kept.data_ptr() if kept is not None else None
+                if not (0 <= b <= e <= plan.P):
+                    raise ValueError("bad compression layer")
+            kp = plan.counter if compress is not None else None
             if tf1:
-                _lib.call("cfa_mix_tf1_f32", ob, hb, table, _lib.double_array([float(a) for a in alphas]),
-                          n, P, int(mode), int(b), int(e), kp, sh)
+                rc = lib.cfa_mix_tf1_f32(plan.ob, plan.hb, plan.table, plan.coeffs(alphas, True), n, plan.P,
+                                         int(mode), int(b), int(e), kp, sh)
+                name = "cfa_mix_tf1_f32"
             else:
-                _lib.call("cfa_mix_seq_compress_f32", ob, hb, table, _lib.float_array(list(alphas)),
-                          n, P, int(mode), int(b), int(e), kp, sh)
+                rc = lib.cfa_mix_seq_compress_f32(plan.ob, plan.hb, plan.table, plan.coeffs(alphas), n, plan.P,
+                                                  int(mode), int(b), int(e), kp, sh)
+                name = "cfa_mix_seq_compress_f32"
         elif divisors is not None:
-            _lib.call("cfa_mix_seq_div_f32", ob, hb, table, _lib.float_array(list(alphas)),
-                      _lib.float_array(list(divisors)), n, P, sh)
+            rc = lib.cfa_mix_seq_div_f32(plan.ob, plan.hb, plan.table, plan.coeffs(alphas),
+                                         _lib.float_array(list(divisors)), n, plan.P, sh)
+            name = "cfa_mix_seq_div_f32"
         else:
-            _lib.call("cfa_mix_seq_f32", ob, hb, table, _lib.float_array(list(alphas)), n, P, sh)
-        kept_n = None
-        if kept is not None:
-            with torch.cuda.stream(st):
-                h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
-                h_cnt.copy_(kept, non_blocking=True)
-        st.synchronize()
-        if kept is not None:
-            kept_n = int(h_cnt.numpy()[0])
-        return layout.unpack(h_out.numpy().copy(), copy=False), kept_n  # the pinned buffer is reused
+            rc = lib.cfa_mix_seq_f32(plan.ob, plan.hb, plan.table, plan.coeffs(alphas), n, plan.P, sh)
+            name = "cfa_mix_seq_f32"
+        if rc != _lib.CFA_OK and compress is not None:
+            plan.reset_count()
+        _lib.check(name, rc)
+        if compress is not None:
+            plan.fetch_count(sh)
+        _lib.check("cfa_stream_synchronize", lib.cfa_stream_synchronize(sh))
+        kept_n = int(plan.count_host[0]) if compress is not None else None
+        return plan.unpack(), kept_n
 
     def _aux_streams(self):
         s = getattr(self._tls, "aux", None)
@@ -408,32 +433,27 @@ class HostMixer:
         if n == 0:
             raise ValueError("mix_tf1 needs at least one neighbour model")
         _check_coefficients(n, alphas)
-        layout = BucketLayout.of(local)
+        layout = _layout_of(local)
         P = layout.P
-        flags = [np.asarray(local[k]).dtype == np.float32 and np.asarray(nbrs[0][k]).dtype == np.float32
-                 for k in range(len(local))]
+        flags = tuple(np.asarray(local[k]).dtype == np.float32 and np.asarray(nbrs[0][k]).dtype == np.float32
+                      for k in range(len(local)))
         st = self._stream()
-        zc = TF1_ZERO_COPY
-        # zero-copy rows keep a pitch of an even number of fp64 (16-byte aligned rows, so the
-        # kernel's vector path applies for odd P too); the staged path copies rows of exactly P
-        pitch = P + (P & 1) if zc else P
+        if TF1_ZERO_COPY:
+            return self._mix_tf1_zero_copy(layout, local, nbrs, alphas, compress, flags, st)
         with torch.cuda.stream(st):
-            host = self._cached("h_in64", (n + 1) * pitch, torch.float64, pinned=True)
-            hv = host.numpy().reshape(n + 1, pitch)
-            layout.pack(local, hv[0, :P])
+            host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
+            hv = host.numpy().reshape(n + 1, P)
+            layout.pack(local, hv[0])
             for j, x in enumerate(nbrs):
                 if callable(x):  # a filler writes the flat bucket itself (e.g. a payload decoder)
-                    x(hv[j + 1, :P])
+                    x(hv[j + 1])
                 else:
-                    layout.pack(x, hv[j + 1, :P])
+                    layout.pack(x, hv[j + 1])
             h_out = self._cached("h_out64", P, torch.float64, pinned=True)
-            if zc:  # the kernel reads the pinned rows and writes the pinned output in place
-                hb, ob = self.engine.host_device_ptr(host), self.engine.host_device_ptr(h_out)
-            else:
-                dev = self._cached("d_in64", (n + 1) * P, torch.float64)
-                dev.copy_(host, non_blocking=True)
-                d = dev.view(n + 1, P)
-                out = self._cached("d_out64", P, torch.float64)
+            dev = self._cached("d_in64", (n + 1) * P, torch.float64)
+            dev.copy_(host, non_blocking=True)
+            d = dev.view(n + 1, P)
+            out = self._cached("d_out64", P, torch.float64)
             mode, cb, ce, kept = 0, 0, 0, None
             if compress is not None:
                 mode, layer = compress
@@ -444,19 +464,11 @@ class HostMixer:
                 b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
                 lo, hi = max(cb, b), min(ce, e)
                 hit = kept is not None and lo < hi
-                if zc:
-                    _lib.call("cfa_mix_tf1_f64", ob + 8 * b, hb + 8 * b,
-                              _lib.ptr_table([hb + 8 * (j * pitch + b) for j in range(1, n + 1)]),
-                              _lib.double_array([float(a) for a in alphas]), n, int(bool(f32)), e - b,
-                              mode if hit else 0, lo - b if hit else 0, hi - b if hit else 0,
-                              kept.data_ptr() if hit else None, self.engine.stream_handle(st))
-                else:
-                    self.engine.mix_tf1_f64(out[b:e], d[0, b:e], [d[j, b:e] for j in range(1, n + 1)],
-                                            [float(a) for a in alphas], f32, mode if hit else 0,
-                                            lo - b if hit else 0, hi - b if hit else 0,
-                                            kept if hit else None, stream=st)
-            if not zc:
-                h_out.copy_(out, non_blocking=True)
+                self.engine.mix_tf1_f64(out[b:e], d[0, b:e], [d[j, b:e] for j in range(1, n + 1)],
+                                        [float(a) for a in alphas], f32, mode if hit else 0,
+                                        lo - b if hit else 0, hi - b if hit else 0,
+                                        kept if hit else None, stream=st)
+            h_out.copy_(out, non_blocking=True)
             if kept is not None:
                 h_cnt = self._cached("h_cnt", 1, torch.int64, pinned=True)
                 h_cnt.copy_(kept, non_blocking=True)
@@ -464,6 +476,35 @@ class HostMixer:
             flat = h_out.numpy().copy()
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
+
+    def _mix_tf1_zero_copy(self, layout, local, nbrs, alphas, compress, flags, st):
+        """mix_tf1 on pinned fp64 rows read and written in place by the kernel (rows of an even
+        number of fp64, so 16-byte aligned for odd P too); one launch per run of layers with
+        the same step-0 precision; the compression count comes back by one 8-byte copy."""
+        n = len(nbrs)
+        plan = self._zc_plan("f64", tuple(layout.shapes), n, np.float64)
+        plan.pack(local, nbrs)
+        sh = plan.stream_handle(st)
+        mode, cb, ce = 0, 0, 0
+        if compress is not None:
+            mode, layer = compress
+            cb, ce = layout.segment(layer)
+        coeffs = plan.coeffs(alphas, True)
+        for k0, k1, f32 in plan.runs(flags):
+            b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
+            lo, hi = max(cb, b), min(ce, e)
+            hit = compress is not None and lo < hi
+            rc = plan.lib.cfa_mix_tf1_f64(plan.ob + 8 * b, plan.hb + 8 * b, plan.run_table(b), coeffs, n,
+                                          int(bool(f32)), e - b, mode if hit else 0, lo - b if hit else 0,
+                                          hi - b if hit else 0, plan.counter if hit else None, sh)
+            if rc != _lib.CFA_OK and compress is not None:
+                plan.reset_count()
+            _lib.check("cfa_mix_tf1_f64", rc)
+        if compress is not None:
+            plan.fetch_count(sh)
+        _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
+        kept_n = int(plan.count_host[0]) if compress is not None else None
+        return plan.unpack(), kept_n
 
     def fold64(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float], rule: int,
                divisors: Optional[Sequence[float]] = None) -> List[np.ndarray]:
@@ -535,6 +576,107 @@ class HostMixer:
         u32 = lambda k: bool(flags[k] & (TF1_STATE_F32 if use_filtered else TF1_GRAD_F32))
         return [w.astype(np.float32) if (n == 0 or (flags[k] & TF1_W_F32 and u32(k))) and f32(W[k]) else w
                 for k, w in enumerate(layout.unpack(W_out, copy=False))]
+
+
+class _ZeroCopyPlan:
+    """Reusable zero-copy state of one layout and fan-in on one thread (see HostMixer._zc_plan).
+
+    Rows of ``pitch`` elements (16-byte multiples) in one pinned buffer: row 0 the local model,
+    rows 1..n the neighbours; the output is a separate pinned row. The kernel reads and writes
+    them through their device addresses over PCIe. ``views[m][k]`` is layer k of row m (flat),
+    so a pack is one ``np.copyto`` per layer, with the same dtype conversion as
+    ``BucketLayout.pack``."""
+
+    def __init__(self, mixer: "HostMixer", shapes: tuple, n: int, dtype):
+        self.layout = BucketLayout(shapes)
+        self.P, self.n = self.layout.P, n
+        self.dtype = np.dtype(dtype)
+        align = 16 // self.dtype.itemsize
+        self.pitch = self.P + (-self.P) % align
+        tdt = torch.float32 if self.dtype == np.float32 else torch.float64
+        self.host = torch.empty(max((n + 1) * self.pitch, 1), dtype=tdt, pin_memory=True)
+        self.out = torch.empty(max(self.P, 1), dtype=tdt, pin_memory=True)
+        hv = self.host.numpy()[:(n + 1) * self.pitch].reshape(n + 1, self.pitch)
+        self.rows = hv
+        segs = [self.layout.segment(k) for k in range(len(shapes))]
+        self.views = [[hv[m, b:e] for b, e in segs] for m in range(n + 1)]
+        self.out_np = self.out.numpy()[:self.P]
+        self.out_slices = [(slice(b, e), shp) for (b, e), shp in zip(segs, self.layout.shapes)]
+        eng = mixer.engine
+        self.hb, self.ob = eng.host_device_ptr(self.host), eng.host_device_ptr(self.out)
+        isz = self.dtype.itemsize
+        self.table = _lib.ptr_table([self.hb + isz * self.pitch * (j + 1) for j in range(n)])
+        self.lib = _lib.load()
+        self._coeffs = {}
+        self._tables = {}
+        self._runs = {}
+        self._sh = None
+        # compression count: a device counter (kernel atomics), read back by one 8-byte copy
+        # into a pinned word and re-zeroed in the same stream order (cfa_counter_fetch)
+        self.counter_t = torch.zeros(1, dtype=torch.int64, device=eng.device)
+        torch.cuda.synchronize(eng.device)
+        self.counter = self.counter_t.data_ptr()
+        self.count_pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self.count_host = self.count_pinned.numpy()
+
+    def stream_handle(self, st) -> int:
+        if self._sh is None or self._sh[0] is not st:
+            self._sh = (st, int(st.cuda_stream))
+        return self._sh[1]
+
+    def coeffs(self, alphas, f64: bool = False):
+        key = (tuple(alphas), f64)
+        arr = self._coeffs.get(key)
+        if arr is None:
+            if len(self._coeffs) >= 64:
+                self._coeffs.clear()
+            arr = self._coeffs[key] = (_lib.double_array([float(a) for a in alphas]) if f64
+                                       else _lib.float_array(list(alphas)))
+        return arr
+
+    def runs(self, flags: tuple):
+        """HostMixer._runs(flags), cached per flag pattern."""
+        r = self._runs.get(flags)
+        if r is None:
+            r = self._runs[flags] = HostMixer._runs(list(flags))
+        return r
+
+    def run_table(self, b: int):
+        """Neighbour pointer table of the element offset ``b`` (one launch per dtype run)."""
+        t = self._tables.get(b)
+        if t is None:
+            isz = self.dtype.itemsize
+            t = self._tables[b] = _lib.ptr_table([self.hb + isz * (self.pitch * (j + 1) + b)
+                                                  for j in range(self.n)])
+        return t
+
+    def pack(self, local, nbrs) -> None:
+        sizes = self.layout.sizes
+        for m, model in enumerate([local] + list(nbrs)):
+            if callable(model):  # a filler writes the flat bucket itself (e.g. a payload decoder)
+                model(self.rows[m, :self.P])
+                continue
+            if len(model) != len(sizes):
+                raise ValueError(f"expected {len(sizes)} tensors, got {len(model)}")
+            for k, (v, a) in enumerate(zip(self.views[m], model)):
+                a = np.asarray(a)
+                if a.size != sizes[k]:
+                    raise ValueError(f"tensor {k} has {a.size} elements, layout expects {sizes[k]}")
+                np.copyto(v, a.reshape(-1), casting="unsafe")
+
+    def fetch_count(self, sh: int) -> None:
+        """Stream-ordered: the device counter's value into ``count_host`` and the counter reset
+        (cfa_counter_fetch); the value is valid after the stream synchronisation."""
+        _lib.check("cfa_counter_fetch", self.lib.cfa_counter_fetch(self.counter, self.count_pinned.data_ptr(), sh))
+
+    def reset_count(self) -> None:
+        """After a failed call: the counter may hold a partial sum; zero it (synchronously)."""
+        self.counter_t.zero_()
+        torch.cuda.synchronize(self.counter_t.device)
+
+    def unpack(self) -> List[np.ndarray]:
+        flat = self.out_np.copy()  # the pinned row is reused by the next call
+        return [flat[sl].reshape(shp) for sl, shp in self.out_slices]
 
 
 _mixers = {}

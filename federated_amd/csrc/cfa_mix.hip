@@ -35,6 +35,17 @@ extern "C" int cfa_device_prepare(int device) {
   if (device != prev) CFA_HIP_CHECK(hipSetDevice(prev));
   return rc;
 }
+extern "C" int cfa_stream_synchronize(void* stream) {
+  CFA_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return CFA_OK;
+}
+extern "C" int cfa_counter_fetch(unsigned long long* counter, unsigned long long* host_dst, void* stream) {
+  if (!counter || !host_dst) return fail(CFA_E_INVALID, "null counter or destination");
+  hipStream_t st = (hipStream_t)stream;
+  CFA_HIP_CHECK(hipMemcpyAsync(host_dst, counter, sizeof(*counter), hipMemcpyDefault, st));
+  CFA_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(*counter), st));
+  return CFA_OK;
+}
 extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }
 // Used by cfa_comm.cpp so every translation unit reports through one thread-local message.
 extern "C" __attribute__((visibility("hidden"))) void cfa_internal_set_error(const char* msg) {

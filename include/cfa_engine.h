@@ -116,6 +116,12 @@ CFA_API const char* cfa_last_error(void);
  * calling thread's current device is restored. Idempotent. */
 CFA_API int cfa_device_prepare(int device);
 
+/* Host-path helpers (the per-call drop-in path): hipStreamSynchronize, and a
+ * stream-ordered fetch of a device uint64 counter (e.g. a compression kept_count) into host
+ * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero. */
+CFA_API int cfa_stream_synchronize(void* stream);
+CFA_API int cfa_counter_fetch(unsigned long long* counter, unsigned long long* host_dst, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.
  *   out[i] = fold_j( w <- w + alphas[j] * (nbrs[j][i] - w) ), w0 = local[i]
