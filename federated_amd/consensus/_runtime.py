@@ -82,6 +82,12 @@ def _check_coefficients(n: int, alphas, divisors=None) -> None:
 
 
 _layouts: dict = {}
+_F32 = np.dtype(np.float32)
+
+
+def _dtype(a):
+    """dtype of an array-like (ndarray fast path)."""
+    return a.dtype if isinstance(a, np.ndarray) else np.asarray(a).dtype
 
 
 def _layout_of(arrays) -> BucketLayout:
@@ -205,18 +211,19 @@ class HostMixer:
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
-    def _zc_plan(self, kind: str, layout_key: tuple, n: int, dtype) -> "_ZeroCopyPlan":
-        """Per-thread cached zero-copy plan for one (kind, layer shapes, fan-in): the layout,
-        pinned rows and output, their device addresses and the ctypes tables, built once."""
+    def _zc_plan(self, kind: str, layout: BucketLayout, n: int, dtype) -> "_ZeroCopyPlan":
+        """Per-thread cached zero-copy plan for one (kind, layout, fan-in): pinned rows and
+        output, their device addresses and the ctypes tables, built once. ``layout`` is a cached
+        ``_layout_of`` object, so it identifies the layer shapes."""
         plans = getattr(self._tls, "plans", None)
         if plans is None:
             plans = self._tls.plans = {}
-        key = (kind, layout_key, n)
+        key = (kind, id(layout), n)
         plan = plans.get(key)
-        if plan is None:
+        if plan is None or plan.layout is not layout:
             if len(plans) >= 16:  # bounded: drop the oldest layout
                 plans.pop(next(iter(plans)))
-            plan = plans[key] = _ZeroCopyPlan(self, layout_key, n, dtype)
+            plan = plans[key] = _ZeroCopyPlan(self, layout, n, dtype)
         return plan
 
     def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st,
@@ -228,7 +235,7 @@ class HostMixer:
         copy (cfa_counter_fetch, which also re-zeroes it). Everything but the pack, the launch
         and the unpack is prepared once per layout (``_ZeroCopyPlan``)."""
         n = len(nbrs)
-        plan = self._zc_plan("f32", tuple(layout.shapes), n, np.float32)
+        plan = self._zc_plan("f32", layout, n, np.float32)
         plan.pack(local, nbrs)
         sh = plan.stream_handle(st)
         lib = plan.lib
@@ -435,7 +442,8 @@ class HostMixer:
         _check_coefficients(n, alphas)
         layout = _layout_of(local)
         P = layout.P
-        flags = tuple(np.asarray(local[k]).dtype == np.float32 and np.asarray(nbrs[0][k]).dtype == np.float32
+        first = nbrs[0]
+        flags = tuple(_dtype(local[k]) == _F32 and not callable(first) and _dtype(first[k]) == _F32
                       for k in range(len(local)))
         st = self._stream()
         if TF1_ZERO_COPY:
@@ -482,7 +490,7 @@ class HostMixer:
         number of fp64, so 16-byte aligned for odd P too); one launch per run of layers with
         the same step-0 precision; the compression count comes back by one 8-byte copy."""
         n = len(nbrs)
-        plan = self._zc_plan("f64", tuple(layout.shapes), n, np.float64)
+        plan = self._zc_plan("f64", layout, n, np.float64)
         plan.pack(local, nbrs)
         sh = plan.stream_handle(st)
         mode, cb, ce = 0, 0, 0
@@ -587,8 +595,9 @@ class _ZeroCopyPlan:
     so a pack is one ``np.copyto`` per layer, with the same dtype conversion as
     ``BucketLayout.pack``."""
 
-    def __init__(self, mixer: "HostMixer", shapes: tuple, n: int, dtype):
-        self.layout = BucketLayout(shapes)
+    def __init__(self, mixer: "HostMixer", layout: BucketLayout, n: int, dtype):
+        self.layout = layout
+        shapes = layout.shapes
         self.P, self.n = self.layout.P, n
         self.dtype = np.dtype(dtype)
         align = 16 // self.dtype.itemsize

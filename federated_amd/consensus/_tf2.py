@@ -99,55 +99,69 @@ class TF2Base:
         self.local_weights = model
         self.layers = self.local_weights.size
 
-    # -- v2/v3 neighbour loading loop (consensus_v3.py:82-141) --------------------------------
-    def _collect_v3(self, neighbor, neighbors, epoch_count, max_lag, model_tpl):
-        """Returns the loaded neighbour models (in order) following the reference loop exactly:
-        status file poll, one retry, ``pause(round(np.random.random(), 2))``, staleness wait
-        (neighbour count < local count - max_lag and not training_end), model load with one
-        retry, early stop after a neighbour that reports training_end."""
-        stop_federation = False
-        loaded = []
-        for q in range(neighbors):
-            outfile_models = model_tpl.format(neighbor[q])
-            outfile = "results/dump_train_variables{}.npz".format(neighbor[q])
-            while not os.path.isfile(outfile):
-                print("waiting for variables")
-                pause(1)
+    # -- the file protocol shared by v2/v3 (consensus_v3.py:82-141) and v4 (consensus_v4.py:30-95)
+    def _read_status(self, outfile):
+        """Poll for a neighbour's status file, load (count, training_end) with one retry.
+        Returns (ok, count); ok False after the second failure ("halting federation")."""
+        while not os.path.isfile(outfile):
+            print("waiting for variables")
+            pause(1)
+        try:
+            nbr_count, self.training_end = _load_vars(outfile, self.count_key)
+        except Exception:
+            pause(5)
+            print("retrying opening variables")
             try:
                 nbr_count, self.training_end = _load_vars(outfile, self.count_key)
             except Exception:
-                pause(5)
+                print("halting federation")
+                return False, None
+        return True, nbr_count
+
+    def _wait_and_load(self, outfile, outfile_models, nbr_count, epoch_count, max_lag):
+        """Staleness wait (neighbour count < local count - max_lag and not training_end, status
+        re-read each second with one retry), then the model load with one retry. Returns
+        (model, success)."""
+        while not os.path.isfile(outfile_models) or nbr_count < epoch_count - max_lag and not self.training_end:
+            pause(1)
+            try:
+                nbr_count, self.training_end = _load_vars(outfile, self.count_key)
+            except Exception:
+                pause(2)
                 print("retrying opening variables")
                 try:
                     nbr_count, self.training_end = _load_vars(outfile, self.count_key)
                 except Exception:
-                    print("halting federation")
-                    stop_federation = True
-                    break
+                    print("problems loading variables")
+        try:
+            return np.load(outfile_models, allow_pickle=True), True
+        except Exception:
+            pause(5)
+            print("retrying opening model")
+            try:
+                return np.load(outfile_models, allow_pickle=True), True
+            except Exception:
+                print("failed to load model federation")
+                return [], False
+
+    def _collect_v3(self, neighbor, neighbors, epoch_count, max_lag, model_tpl):
+        """Returns the loaded neighbour models (in order) following the reference loop exactly:
+        status file poll, one retry (a second failure stops the loop), ``pause(round(
+        np.random.random(), 2))``, staleness wait, model load with one retry, early stop after a
+        neighbour that reports training_end."""
+        loaded = []
+        for q in range(neighbors):
+            outfile_models = model_tpl.format(neighbor[q])
+            outfile = "results/dump_train_variables{}.npz".format(neighbor[q])
+            ok, nbr_count = self._read_status(outfile)
+            if not ok:
+                break
             pause(round(np.random.random(), 2))
-            if not stop_federation:
-                while not os.path.isfile(outfile_models) or nbr_count < epoch_count - max_lag and not self.training_end:
-                    pause(1)
-                    try:
-                        nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-                    except Exception:
-                        pause(2)
-                        print("retrying opening variables")
-                        try:
-                            nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-                        except Exception:
-                            print("problems loading variables")
-                try:
-                    loaded.append(np.load(outfile_models, allow_pickle=True))
-                except Exception:
-                    pause(5)
-                    print("retrying opening model")
-                    try:
-                        loaded.append(np.load(outfile_models, allow_pickle=True))
-                    except Exception:
-                        print("failed to load model federation")
-                if self.training_end and len(loaded) > 0:
-                    break
+            model, success = self._wait_and_load(outfile, outfile_models, nbr_count, epoch_count, max_lag)
+            if success:
+                loaded.append(model)
+            if self.training_end and len(loaded) > 0:
+                break
         return loaded
 
     def _apply_weights(self, loaded):

@@ -5,65 +5,28 @@ caller's eps. Reference call site: ..._CIFAR100_gradients_exchange.py:393-457.
 """
 from __future__ import annotations
 
-import os
 import warnings
 
 import numpy as np
 
 from ._runtime import pause
-from ._tf2 import TF2Base, _load_vars, _mix_into, kregular_ring, to_tensors, tx_ring
+from ._tf2 import TF2Base, _mix_into, kregular_ring, to_tensors, tx_ring
 
 
 class CFA_process(TF2Base):
     count_key = "epoch_count"
 
     def get_neighbor_weights(self, epoch_count, outfile, outfile_models, epoch=0, max_lag=1):
-        """consensus_v4.py:30-95: status poll (one retry), ``pause(round(np.random.random(), 2))``,
-        staleness wait, model load with one retry. Returns (model, success)."""
+        """consensus_v4.py:30-95, on the shared protocol helpers of ``TF2Base``: status poll
+        (one retry), ``pause(round(np.random.random(), 2))`` (drawn even after a failed status
+        read, as the reference does), staleness wait, model load with one retry. Returns
+        (model, success)."""
         warnings.filterwarnings("ignore")
-        success = False
-        stop_federation = False
-        while not os.path.isfile(outfile):
-            print("waiting for variables")
-            pause(1)
-        try:
-            nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-        except Exception:
-            pause(5)
-            print("retrying opening variables")
-            try:
-                nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-            except Exception:
-                print("halting federation")
-                stop_federation = True
+        ok, nbr_count = self._read_status(outfile)
         pause(round(np.random.random(), 2))
-        if not stop_federation:
-            while not os.path.isfile(outfile_models) or nbr_count < epoch_count - max_lag and not self.training_end:
-                pause(1)
-                try:
-                    nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-                except Exception:
-                    pause(2)
-                    print("retrying opening variables")
-                    try:
-                        nbr_count, self.training_end = _load_vars(outfile, self.count_key)
-                    except Exception:
-                        print("problems loading variables")
-            try:
-                neighbor_model = np.load(outfile_models, allow_pickle=True)
-                success = True
-            except Exception:
-                pause(5)
-                print("retrying opening model")
-                try:
-                    neighbor_model = np.load(outfile_models, allow_pickle=True)
-                    success = True
-                except Exception:
-                    print("failed to load model federation")
-                    neighbor_model = []
-        else:
-            neighbor_model = []
-        return neighbor_model, success
+        if not ok:
+            return [], False
+        return self._wait_and_load(outfile, outfile_models, nbr_count, epoch_count, max_lag)
 
     def get_connectivity(self, ii_saved_local, neighbors, devices):
         """consensus_v4.py:111-141."""

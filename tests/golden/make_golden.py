@@ -148,6 +148,7 @@ def case_tf1_cfa():
     out = {}
     specs = [  # (tag, shapes, devices, N, eps, devices under test)
         ("2nn_K5_N2_eps1", SHAPES_2NN, 5, 2, 1.0, (0, 2, 4)),
+        ("2nn_K4_N2_eps1", SHAPES_2NN, 4, 2, 1.0, (0, 1, 2, 3)),  # config 1: federated_sample_2NN_CFA.py:107
         ("cnn_K5_N2_eps05", SHAPES_CNN_GE, 5, 2, 0.5, (2,)),
         ("cnn_K5_N3_eps1", SHAPES_CNN_GE, 5, 3, 1.0, (0, 2, 4)),
         ("cnn_K8_N4_eps07", SHAPES_CNN_GE, 8, 4, 0.7, (0, 1, 3, 7)),
@@ -530,7 +531,7 @@ def case_topology():
     v3 = load_v3()
     v4 = load_ref(os.path.join(TF2, "MNIST_dataset", "consensus", "consensus_v4.py"), "ref_tf2_v4_topo")
     rows = {"tf1": [], "v3": [], "v4": [], "v4tx": []}
-    for K in (5, 8, 16, 32, 128):
+    for K in (4, 5, 8, 16, 32, 128):  # K = 4: config 1's population
         for N in (1, 2, 3, 4):
             p1 = cfa.CFA_process(True, K, 0, N)
             p3 = v3.CFA_process(K, 0, N)

@@ -32,7 +32,7 @@ def _tf1_models(z, tag, prefix, dev):
     return [z[f"{tag}/{prefix}_{t}"][dev] for t in range(4)]
 
 
-@pytest.mark.parametrize("tag", ["2nn_K5_N2_eps1", "cnn_K5_N2_eps05", "cnn_K5_N3_eps1", "cnn_K8_N4_eps07"])
+@pytest.mark.parametrize("tag", ["2nn_K5_N2_eps1", "2nn_K4_N2_eps1", "cnn_K5_N2_eps05", "cnn_K5_N3_eps1", "cnn_K8_N4_eps07"])
 def test_tf1_cfa_oracle_bitexact(tag):
     z = load_golden("tf1_cfa.npz")
     K, N = (int(x) for x in z[f"{tag}/meta"])
