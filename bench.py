@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="PMC traffic summary (default profiles/r01_pmc_traffic.json, or "
                         "profiles/r01_window_pmc_traffic.json with --window-batch)")
+    p.add_argument("--no-live-traffic", action="store_true",
+                   help="N = 1: do not measure roofline.traffic with rocprofv3 PMC passes in this run "
+                        "(the committed profiles/ value is reported instead)")
     p.add_argument("--e2e", action="store_true",
                    help="also measure the host-resident path (pinned H2D + mix + D2H) on rank 0")
     return p.parse_args()
@@ -194,6 +197,44 @@ def load_traffic(path: str, P: int, K: int, kernel: str = None, devices_per_laun
             and t.get("devices_per_launch", 1) == devices_per_launch):
         return t.get("hbm_bytes_per_launch")
     return None
+
+
+def live_traffic(P: int, K: int, timeout: float = 150.0):
+    """HBM bytes per launch of the dominant kernel, measured in THIS run: two rocprofv3 PMC passes
+    (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over a child process that
+    launches the same kernel on the same bucket shape (tools/pmc_probe.py), corrected as
+    MI355X_MICROARCH.md prescribes (KiB; gfx950 FETCH_SIZE counts half of a wide coalesced
+    read). Returns (bytes, note) or (None, reason) when the profiler is unavailable."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import per_dispatch
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not on PATH"
+    vals = {}
+    with tempfile.TemporaryDirectory(prefix="cfa_pmc_") as d:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = [prof, "--pmc", counter, "-d", os.path.join(d, counter), "-o", "pmc", "--output-format", "csv",
+                   "--", sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), "--params", str(P),
+                   "--neighbours", str(K)]
+            try:
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 {counter} pass timed out"
+            files = glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return None, f"rocprofv3 {counter} pass failed (rc {r.returncode})"
+            per = per_dispatch(files[0], counter, KERNEL)
+            if not per:
+                return None, f"no {KERNEL} dispatch in the {counter} pass"
+            vals[counter] = statistics.median(per)
+    read = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return read + write, ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run (tools/pmc_probe.py, "
+                          "median over the launches), read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB")
 
 
 class TransportError(RuntimeError):
@@ -475,6 +516,14 @@ def main():
                 result["cpu_baseline_pool"] = cpu_baseline_pool(P, K, D, args.cpu_pool_seconds)
         else:
             result["cpu_baseline"] = None
+        if world == 1 and not args.no_live_traffic and not args.window_batch:
+            live, note = live_traffic(shard_P(info, P), K)
+            rl = result["roofline"]
+            if live is not None:
+                rl["traffic_committed"] = rl["traffic"]
+                rl["traffic"] = round(live, 1)
+                rl["traffic_over_algorithmic"] = round(live / rl["bytes_per_launch"], 5)
+            rl["traffic_source"] = note if live is not None else f"committed profile ({note})"
         if args.e2e:
             from federated_amd.staging import measure_e2e
             result["e2e"] = measure_e2e(eng, P, K)
