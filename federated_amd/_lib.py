@@ -66,6 +66,8 @@ SIGNATURES = {
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,
                                     _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p, _c_void_p]),
+    "cfa_mix_tf1_wide_f32": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int,
+                                      _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_mix_tf1_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double), _c_int, _c_int,
                                  _c_size_t, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p]),
     "cfa_fold_f64": (_c_int, [_c_void_p, _c_void_p, _PP, ctypes.POINTER(ctypes.c_double),

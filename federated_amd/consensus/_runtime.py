@@ -211,7 +211,7 @@ class HostMixer:
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
 
-    def _zc_plan(self, kind: str, layout: BucketLayout, n: int, dtype) -> "_ZeroCopyPlan":
+    def _zc_plan(self, kind: str, layout: BucketLayout, n: int, dtype, out_dtype=None) -> "_ZeroCopyPlan":
         """Per-thread cached zero-copy plan for one (kind, layout, fan-in): pinned rows and
         output, their device addresses and the ctypes tables, built once. ``layout`` is a cached
         ``_layout_of`` object, so it identifies the layer shapes."""
@@ -223,7 +223,7 @@ class HostMixer:
         if plan is None or plan.layout is not layout:
             if len(plans) >= 16:  # bounded: drop the oldest layout
                 plans.pop(next(iter(plans)))
-            plan = plans[key] = _ZeroCopyPlan(self, layout, n, dtype)
+            plan = plans[key] = _ZeroCopyPlan(self, layout, n, dtype, out_dtype)
         return plan
 
     def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st,
@@ -447,6 +447,8 @@ class HostMixer:
                       for k in range(len(local)))
         st = self._stream()
         if TF1_ZERO_COPY:
+            if all(flags) and all(not callable(x) and all(_dtype(a) == _F32 for a in x) for x in nbrs[1:]):
+                return self._mix_tf1_wide(layout, local, nbrs, alphas, compress, st)
             return self._mix_tf1_zero_copy(layout, local, nbrs, alphas, compress, flags, st)
         with torch.cuda.stream(st):
             host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
@@ -484,6 +486,31 @@ class HostMixer:
             flat = h_out.numpy().copy()
             kept_n = int(h_cnt.numpy()[0]) if kept is not None else None
         return layout.unpack(flat, copy=False), kept_n
+
+    def _mix_tf1_wide(self, layout, local, nbrs, alphas, compress, st):
+        """mix_tf1 when every array is fp32 (what TF hands the TF1 drivers): fp32 pinned rows, one
+        cfa_mix_tf1_wide_f32 launch writing the unrounded fp64 result into a pinned fp64 row.
+        The same values as the fp64-row path (fp32 values widen exactly; step 0 is the fp32
+        subtraction there too) at half the packed and PCIe-read bytes."""
+        n = len(nbrs)
+        plan = self._zc_plan("tf1w", layout, n, np.float32, out_dtype=np.float64)
+        plan.pack(local, nbrs)
+        sh = plan.stream_handle(st)
+        mode, cb, ce = 0, 0, 0
+        if compress is not None:
+            mode, layer = compress
+            cb, ce = layout.segment(layer)
+        rc = plan.lib.cfa_mix_tf1_wide_f32(plan.ob, plan.hb, plan.table, plan.coeffs(alphas, True), n, plan.P,
+                                           int(mode), int(cb), int(ce),
+                                           plan.counter if compress is not None else None, sh)
+        if rc != _lib.CFA_OK and compress is not None:
+            plan.reset_count()
+        _lib.check("cfa_mix_tf1_wide_f32", rc)
+        if compress is not None:
+            plan.fetch_count(sh)
+        _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
+        kept_n = int(plan.count_host[0]) if compress is not None else None
+        return plan.unpack(), kept_n
 
     def _mix_tf1_zero_copy(self, layout, local, nbrs, alphas, compress, flags, st):
         """mix_tf1 on pinned fp64 rows read and written in place by the kernel (rows of an even
@@ -595,16 +622,16 @@ class _ZeroCopyPlan:
     so a pack is one ``np.copyto`` per layer, with the same dtype conversion as
     ``BucketLayout.pack``."""
 
-    def __init__(self, mixer: "HostMixer", layout: BucketLayout, n: int, dtype):
+    def __init__(self, mixer: "HostMixer", layout: BucketLayout, n: int, dtype, out_dtype=None):
         self.layout = layout
         shapes = layout.shapes
         self.P, self.n = self.layout.P, n
         self.dtype = np.dtype(dtype)
         align = 16 // self.dtype.itemsize
         self.pitch = self.P + (-self.P) % align
-        tdt = torch.float32 if self.dtype == np.float32 else torch.float64
-        self.host = torch.empty(max((n + 1) * self.pitch, 1), dtype=tdt, pin_memory=True)
-        self.out = torch.empty(max(self.P, 1), dtype=tdt, pin_memory=True)
+        tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+        self.host = torch.empty(max((n + 1) * self.pitch, 1), dtype=tdt[self.dtype], pin_memory=True)
+        self.out = torch.empty(max(self.P, 1), dtype=tdt[np.dtype(out_dtype or dtype)], pin_memory=True)
         hv = self.host.numpy()[:(n + 1) * self.pitch].reshape(n + 1, self.pitch)
         self.rows = hv
         segs = [self.layout.segment(k) for k in range(len(shapes))]

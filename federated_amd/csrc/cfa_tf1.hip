@@ -14,7 +14,8 @@ namespace {
 // TF1 numerics (cfa_mix_tf1_f32): the reference's chain under numpy 2 is fp32 for the first
 // subtraction and fp64 after it (eps * wf is an np.float64), so w is carried in double and
 // rounded to fp32 once, after the (fp64) compression epilogue. Fan-ins above CFA_MAX_FANIN
-// chain passes through an fp64 scratch bucket (FROM64 / TO64).
+// chain passes through an fp64 scratch bucket (FROM64 / kOutScratch64); cfa_mix_tf1_wide_f32
+// writes the unrounded fp64 result instead (and chains its passes in that output).
 // ------------------------------------------------------------------------------------------
 struct Tf1Fanin {
   const float* local;               // pre-mix local: step-0 input and DPCM reference
@@ -23,7 +24,11 @@ struct Tf1Fanin {
   double a[CFA_MAX_FANIN];          // eps * wf_j
 };
 
-template <int N, bool FROM64, bool TO64>
+// Output of a TF1 pass: the fp32 result (epilogue, one rounding), the fp64 scratch of a chained
+// pass (no epilogue), or the unrounded fp64 result (epilogue in fp64, no rounding).
+enum { kOutF32 = 0, kOutScratch64 = 1, kOutF64 = 2 };
+
+template <int N, bool FROM64, int OUT>
 __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin f, long long nvec,
                                                               CompressParams cp, int compress) {
   unsigned kept = 0;
@@ -49,26 +54,26 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin
     for (int j = j0; j < N; ++j)
 #pragma unroll
       for (int c = 0; c < 4; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
-    if constexpr (TO64) {
+    if (OUT != kOutScratch64 && compress) {
+      const long long e0 = i * 4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
+    }
+    if constexpr (OUT == kOutF32) {
+      const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+      st4<true>(reinterpret_cast<float*>(out), i, y);
+    } else {
       double* o = reinterpret_cast<double*>(out) + 4 * i;
 #pragma unroll
       for (int c = 0; c < 4; ++c) o[c] = w[c];
-    } else {
-      if (compress) {
-        const long long e0 = i * 4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
-      }
-      const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
-      st4<true>(reinterpret_cast<float*>(out), i, y);
     }
   }
-  if (!TO64 && compress) block_add_count(kept, cp.kept);
+  if (OUT != kOutScratch64 && compress) block_add_count(kept, cp.kept);
 }
 
 // Scalar TF1 path (misaligned buckets, head and tail pieces).
-__global__ __launch_bounds__(kBlock) void mix_tf1_scalar_kernel(void* out, int to64, Tf1Fanin f,
+__global__ __launch_bounds__(kBlock) void mix_tf1_scalar_kernel(void* out, int out_mode, Tf1Fanin f,
                                                                 int n, long long P,
                                                                 CompressParams cp, int compress) {
   unsigned kept = 0;
@@ -85,14 +90,14 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_scalar_kernel(void* out, int t
       j = 1;
     }
     for (; j < n; ++j) w = w + f.a[j] * ((double)f.src[j][i] - w);
-    if (to64) {
-      reinterpret_cast<double*>(out)[i] = w;
-    } else {
-      if (compress && i >= cp.cbegin && i < cp.cend) w = compress_one_d(w, l, cp, kept);
+    if (out_mode != kOutScratch64 && compress && i >= cp.cbegin && i < cp.cend)
+      w = compress_one_d(w, l, cp, kept);
+    if (out_mode == kOutF32)
       reinterpret_cast<float*>(out)[i] = (float)w;
-    }
+    else
+      reinterpret_cast<double*>(out)[i] = w;
   }
-  if (!to64 && compress) block_add_count(kept, cp.kept);
+  if (out_mode != kOutScratch64 && compress) block_add_count(kept, cp.kept);
 }
 
 // fp64 buckets (cfa_mix_tf1_f64 / cfa_mewma_tf1_f64): the reference's TF1 arrays as they are
@@ -328,12 +333,12 @@ static void launch_mewma_f64_vec(int m, unsigned grid, hipStream_t st, const Mew
   ((m == Ns + 1 ? (void)(mewma_tf1_f64_vec_kernel<Ns + 1><<<grid, kBlock, 0, st>>>(a, nvec2)) : (void)0), ...);
 }
 
-template <bool FROM64, bool TO64>
+template <bool FROM64, int OUT>
 static void launch_tf1_vec(int n, unsigned grid, hipStream_t st, void* out, const Tf1Fanin& f,
                            long long nvec, const CompressParams& cp, int compress) {
 #define CFA_CASE(K) \
   case K:           \
-    mix_tf1_vec_kernel<K, FROM64, TO64><<<grid, kBlock, 0, st>>>(out, f, nvec, cp, compress); \
+    mix_tf1_vec_kernel<K, FROM64, OUT><<<grid, kBlock, 0, st>>>(out, f, nvec, cp, compress); \
     break;
   switch (n) {
     CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6) CFA_CASE(7)
@@ -345,8 +350,9 @@ static void launch_tf1_vec(int n, unsigned grid, hipStream_t st, void* out, cons
 }
 
 // One TF1 pass of 1..CFA_MAX_FANIN neighbours over [0, P): `head` scalar elements, a float4
-// body of nvec vectors, a scalar tail. out is fp32 (last pass) or the fp64 scratch.
-static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
+// body of nvec vectors, a scalar tail. out_mode: kOutF32 (last pass, fp32 out), kOutScratch64
+// (fp64 scratch of a chained pass) or kOutF64 (last pass, unrounded fp64 out).
+static int tf1_pass(void* out, int out_mode, const float* local, const double* w64,
                     const float* const* nbrs, const double* a, int m, size_t P, size_t head,
                     size_t nvec, const CompressParams& cp, int compress, hipStream_t st) {
   auto fanin_at = [&](size_t b) {
@@ -360,7 +366,7 @@ static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
     return f;
   };
   auto out_at = [&](size_t b) -> void* {
-    return to64 ? (void*)((double*)out + b) : (void*)((float*)out + b);
+    return out_mode != kOutF32 ? (void*)((double*)out + b) : (void*)((float*)out + b);
   };
   auto shifted = [&](size_t b) {
     CompressParams c = cp;
@@ -373,10 +379,17 @@ static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
     const unsigned grid = grid_for(((long long)nvec + kBlock - 1) / kBlock);
     const CompressParams c = shifted(head);
     void* o = out_at(head);
-    if (!w64 && !to64) launch_tf1_vec<false, false>(m, grid, st, o, f, (long long)nvec, c, compress);
-    else if (!w64 && to64) launch_tf1_vec<false, true>(m, grid, st, o, f, (long long)nvec, c, compress);
-    else if (w64 && to64) launch_tf1_vec<true, true>(m, grid, st, o, f, (long long)nvec, c, compress);
-    else launch_tf1_vec<true, false>(m, grid, st, o, f, (long long)nvec, c, compress);
+    const long long nv = (long long)nvec;
+    if (out_mode == kOutF32) {
+      if (w64) launch_tf1_vec<true, kOutF32>(m, grid, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutF32>(m, grid, st, o, f, nv, c, compress);
+    } else if (out_mode == kOutScratch64) {
+      if (w64) launch_tf1_vec<true, kOutScratch64>(m, grid, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutScratch64>(m, grid, st, o, f, nv, c, compress);
+    } else {
+      if (w64) launch_tf1_vec<true, kOutF64>(m, grid, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutF64>(m, grid, st, o, f, nv, c, compress);
+    }
     if (int rc = check_launch("mix_tf1_vec")) return rc;
   }
   const size_t tail_begin = head + nvec * 4;
@@ -386,7 +399,7 @@ static int tf1_pass(void* out, bool to64, const float* local, const double* w64,
     if (e <= b) continue;
     const long long len = (long long)(e - b);
     mix_tf1_scalar_kernel<<<grid_for((len + kBlock - 1) / kBlock), kBlock, 0, st>>>(
-        out_at(b), to64 ? 1 : 0, fanin_at(b), m, len, shifted(b), compress);
+        out_at(b), out_mode, fanin_at(b), m, len, shifted(b), compress);
     if (int rc = check_launch("mix_tf1_scalar")) return rc;
   }
   return CFA_OK;
@@ -401,34 +414,36 @@ extern "C" int cfa_mix_tf1_f32(float* out, const float* local, const float* cons
                             stream);
 }
 
-extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* const* nbrs,
-                                  const double* alphas, int n, size_t P, int mode, size_t cbegin,
-                                  size_t cend, unsigned long long* kept_count, double* scratch_in,
-                                  void* stream) {
-  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
-  if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "null kept_count");
+namespace {
+// The TF1 chain over fp32 buckets: out is fp32 (rounded once, out64 false) or fp64 (unrounded).
+int mix_tf1_impl(void* out, bool out64, const float* local, const float* const* nbrs, const double* alphas,
+                 int n, size_t P, int mode, size_t cbegin, size_t cend, unsigned long long* kept_count,
+                 double* scratch_in, hipStream_t st, const char* fn) {
+  if (n > 0 && !alphas) return fail(CFA_E_INVALID, "%s: null alphas", fn);
+  if (mode != CFA_COMPRESS_NONE && !kept_count) return fail(CFA_E_INVALID, "%s: null kept_count", fn);
   // With a counter the epilogue runs (mode 0 keeps, and counts, every element of the range).
-  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "bad compression range");
-  if (int rc = validate_mix(out, local, nbrs, n, P)) return rc;
+  if (cbegin > cend || cend > P) return fail(CFA_E_INVALID, "%s: bad compression range", fn);
+  if (out64 && n == 0) return fail(CFA_E_INVALID, "%s: needs at least one neighbour", fn);
+  // null pointers, and an output that starts at a neighbour bucket (fp32 or fp64 alike)
+  if (int rc = validate_mix(static_cast<const float*>(out), local, nbrs, n, P)) return rc;
   CompressParams cp{};
   if (int rc = compress_params(mode, cp)) return rc;
   cp.cbegin = (long long)cbegin;
   cp.cend = (long long)cend;
   cp.kept = kept_count;
   const int compress = kept_count ? 1 : 0;
-  hipStream_t st = (hipStream_t)stream;
   if (n == 0) {
     // No neighbour: the bucket is the local model (fp32), then the epilogue (cfa_ongraphs.py:218-223).
-    if (out != local && P > 0)
-      CFA_HIP_CHECK(hipMemcpyAsync(out, local, P * sizeof(float), hipMemcpyDefault, st));
+    float* o = static_cast<float*>(out);
+    if (o != local && P > 0)
+      CFA_HIP_CHECK(hipMemcpyAsync(o, local, P * sizeof(float), hipMemcpyDefault, st));
     if (!compress) return CFA_OK;
-    return cfa_compress_epilogue_f32(out + cbegin, local + cbegin, mode, cend - cbegin, kept_count,
-                                     stream);
+    return cfa_compress_epilogue_f32(o + cbegin, local + cbegin, mode, cend - cbegin, kept_count, st);
   }
   if (P == 0) return CFA_OK;
-  // Body/head/tail split shared by every pass (fp32 pointers decide it; the fp64 scratch is
-  // indexed like the bucket and only needs 8-byte alignment).
-  const uintptr_t mis = addr(out) & 15;
+  // Body/head/tail split shared by every pass (the fp32 pointers decide it; fp64 buckets, the
+  // scratch and an fp64 out, are indexed like the bucket and only need 8-byte alignment).
+  const uintptr_t mis = addr(out64 ? (const void*)local : out) & 15;
   bool same = (addr(local) & 15) == mis;
   for (int j = 0; j < n; ++j) same = same && ((addr(nbrs[j]) & 15) == mis);
   size_t head = P, nvec = 0;
@@ -437,15 +452,16 @@ extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* c
     if (head > P) head = P;
     nvec = (P - head) / 4;
   }
-  double* scratch = scratch_in;
+  // chained passes carry w in fp64: in an fp64 out itself, else in the scratch bucket
+  double* scratch = out64 ? static_cast<double*>(out) : scratch_in;
   bool owned = false;
   if (n > CFA_MAX_FANIN && !scratch) {
     // no caller scratch: a stream-ordered allocation, which a hipGraph capture must not contain
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     CFA_HIP_CHECK(hipStreamIsCapturing(st, &cs));
     if (cs != hipStreamCaptureStatusNone)
-      return fail(CFA_E_INVALID, "cfa_mix_tf1_f32: %d > %d neighbours under graph capture need a "
-                  "caller scratch bucket (cfa_mix_tf1_ex_f32)", n, CFA_MAX_FANIN);
+      return fail(CFA_E_INVALID, "%s: %d > %d neighbours under graph capture need a caller scratch "
+                  "bucket (cfa_mix_tf1_ex_f32)", fn, n, CFA_MAX_FANIN);
     CFA_HIP_CHECK(hipMallocAsync((void**)&scratch, P * sizeof(double), st));
     owned = true;
   }
@@ -453,8 +469,9 @@ extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* c
   for (int done = 0; done < n && rc == CFA_OK;) {
     const int m = (n - done) > CFA_MAX_FANIN ? CFA_MAX_FANIN : (n - done);
     const bool last = done + m == n;
-    rc = tf1_pass(last ? (void*)out : (void*)scratch, !last, local, done ? scratch : nullptr,
-                  nbrs + done, alphas + done, m, P, head, nvec, cp, last ? compress : 0, st);
+    const int out_mode = !last ? kOutScratch64 : (out64 ? kOutF64 : kOutF32);
+    rc = tf1_pass(last ? out : (void*)scratch, out_mode, local, done ? scratch : nullptr, nbrs + done,
+                  alphas + done, m, P, head, nvec, cp, last ? compress : 0, st);
     done += m;
   }
   if (owned) {
@@ -462,6 +479,22 @@ extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* c
     if (rc == CFA_OK && e != hipSuccess) return fail(CFA_E_HIP, "hipFreeAsync: %s", hipGetErrorString(e));
   }
   return rc;
+}
+}  // namespace
+
+extern "C" int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* const* nbrs,
+                                  const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                                  size_t cend, unsigned long long* kept_count, double* scratch_in,
+                                  void* stream) {
+  return mix_tf1_impl(out, false, local, nbrs, alphas, n, P, mode, cbegin, cend, kept_count, scratch_in,
+                      (hipStream_t)stream, "cfa_mix_tf1_f32");
+}
+
+extern "C" int cfa_mix_tf1_wide_f32(double* out, const float* local, const float* const* nbrs,
+                                    const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                                    size_t cend, unsigned long long* kept_count, void* stream) {
+  return mix_tf1_impl(out, true, local, nbrs, alphas, n, P, mode, cbegin, cend, kept_count, nullptr,
+                      (hipStream_t)stream, "cfa_mix_tf1_wide_f32");
 }
 
 namespace {

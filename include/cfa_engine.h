@@ -199,6 +199,15 @@ CFA_API int cfa_mix_tf1_f32(float* out, const float* local, const float* const* 
                             const double* alphas, int n, size_t P, int mode, size_t cbegin,
                             size_t cend, unsigned long long* kept_count, void* stream);
 
+/* The same TF1 chain over fp32 buckets, written UNROUNDED into an fp64 `out` (P doubles): the
+ * fp64 arrays the reference itself returns when its inputs are fp32 (cfa.py:66-76 under numpy 2:
+ * fp32 first subtraction, fp64 after; the epilogue in fp64). Equal to cfa_mix_tf1_f64 on the
+ * widened buckets with step0_f32 = 1, at half the input bytes. n >= 1; passes above
+ * CFA_MAX_FANIN chain in `out` itself (no scratch, no allocation). */
+CFA_API int cfa_mix_tf1_wide_f32(double* out, const float* local, const float* const* nbrs,
+                                 const double* alphas, int n, size_t P, int mode, size_t cbegin,
+                                 size_t cend, unsigned long long* kept_count, void* stream);
+
 /* cfa_mix_tf1_f32 with a caller-owned fp64 scratch bucket (device, >= P doubles, 8-byte
  * aligned; used only when n > CFA_MAX_FANIN, may be NULL otherwise): no allocation at all. */
 CFA_API int cfa_mix_tf1_ex_f32(float* out, const float* local, const float* const* nbrs,

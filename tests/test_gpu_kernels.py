@@ -537,3 +537,30 @@ def test_fold_f64_div_quotient_exact_over_exponent_range(gpu, divisors):
             got = out.cpu().numpy()
             same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
             assert same.all(), (C, x[~same][:4], got[~same][:4], ref[~same][:4])
+
+
+@pytest.mark.parametrize("n,P,off,mode", [(2, 16_680, 0, 0), (3, 24_622, 0, 2), (1, 1001, 1, 1), (19, 5003, 0, 3),
+                                          (4, 4099, 3, 4)])
+def test_tf1_wide_equals_f64_rows(gpu, n, P, off, mode):
+    """cfa_mix_tf1_wide_f32 (fp32 rows in, unrounded fp64 out) equals cfa_mix_tf1_f64 on the same
+    rows widened to fp64 with step0_f32 (the reference's numpy-2 chain for fp32 inputs), bit for
+    bit, counts included: misaligned starts, fan-in above CFA_MAX_FANIN (chained in the output)
+    and every compression mode."""
+    from federated_amd import _lib
+    g = torch.Generator(device="cuda").manual_seed(P + n)
+    base = torch.randn((n + 1) * (P + 8), device="cuda", generator=g) * 1e-3
+    rows = [base[j * (P + 8) + off: j * (P + 8) + off + P] for j in range(n + 1)]
+    al = [0.5 / (n + 1)] * n
+    cb, ce = (P // 3, P // 3 + 777) if mode else (0, 0)
+    out_w = torch.full((P + 1,), float("nan"), dtype=torch.float64, device="cuda")[1:] if off else \
+        torch.full((P,), float("nan"), dtype=torch.float64, device="cuda")
+    kw, kf = gpu.counter(), gpu.counter()
+    _lib.call("cfa_mix_tf1_wide_f32", out_w.data_ptr(), rows[0].data_ptr(),
+              _lib.ptr_table([r.data_ptr() for r in rows[1:]]), _lib.double_array(al), n, P, mode, cb, ce,
+              kw.data_ptr() if mode else None, gpu.stream_handle())
+    r64 = [r.double() for r in rows]
+    out_f = torch.empty(P, dtype=torch.float64, device="cuda")
+    gpu.mix_tf1_f64(out_f, r64[0], r64[1:], al, True, mode, cb, ce, kf if mode else None)
+    torch.cuda.synchronize()
+    assert torch.equal(out_w, out_f)
+    assert int(kw.item()) == int(kf.item())
