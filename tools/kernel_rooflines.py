@@ -66,6 +66,13 @@ def main():
         timed(lambda: eng.mix_linear(out, local, nb, [0.1] * (n + 1)), R))
     rec("TF1 rule, fp32 buckets, n=8", "cfa_mix_tf1_f32", (n + 2) * P * 4,
         timed(lambda: eng.mix_tf1(out, local, nb, al), R))
+    o64w = torch.empty(P, device="cuda", dtype=torch.float64)
+    tb = _lib.ptr_table([x.data_ptr() for x in nb])
+    al64 = _lib.double_array(al)
+    rec("TF1 rule, fp32 buckets in, unrounded fp64 out, n=8", "cfa_mix_tf1_wide_f32", (n + 1) * P * 4 + P * 8,
+        timed(lambda: _lib.call("cfa_mix_tf1_wide_f32", o64w.data_ptr(), local.data_ptr(), tb, al64, n, P, 0, 0, 0,
+                                None, eng.stream_handle()), R))
+    del o64w
     kept = eng.counter()
     rec("mix + fused compression (mode 2) on the whole bucket, n=3", "cfa_mix_seq_compress_f32", 5 * P * 4,
         timed(lambda: eng.mix_seq_compress(out, local, nb[:3], al[:3], 2, 0, P, kept), R))
