@@ -336,3 +336,76 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_mult
                                                               tiles, total, f, nvec);
   return check_launch("mix8_multi");
 }
+
+// ------------------------------------------------------------------------------------------
+// Contention experiment (tools/probe/contention.py): how much do the mixes of a round slow down
+// while another kernel holds a few CUs (as RCCL's copy kernels do during a halo exchange), and
+// does handing tiles out dynamically (one device-scope counter, the next tile fetched while the
+// current one streams) recover it? `hog`: `blocks` workgroups copy n float4 `reps` times
+// (bounded work). `mix8_dyn`: the production mix (nt loads, sc1 buffer stores) with dynamic
+// tiles; the counter is zeroed by the host before each launch.
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(kBlock) void hog_kernel(f4* dst, const f4* src, long long n, int reps) {
+  for (int r = 0; r < reps; ++r)
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock)
+      dst[i] = src[i] + (float)r;
+}
+
+__global__ __launch_bounds__(kBlock) void mix8_dyn_kernel(float* out, Fanin f, long long nvec,
+                                                         unsigned long long* counter) {
+  constexpr int N = 8, U = 4;
+  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  __shared__ long long slot[2];
+  if (threadIdx.x == 0) slot[0] = (long long)atomicAdd(counter, 1ull);
+  __syncthreads();
+  long long t = slot[0];
+  int p = 0;
+  while (t < full) {
+    if (threadIdx.x == 0) slot[p ^ 1] = (long long)atomicAdd(counter, 1ull);  // next tile, in flight
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), w,
+                                             (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+    }
+    __syncthreads();
+    p ^= 1;
+    t = slot[p];
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_hog(float* dst, const float* src, size_t n,
+                                                                           int blocks, int reps, void* stream) {
+  if (n % 4 || blocks < 1 || reps < 1) return fail(CFA_E_INVALID, "hog: n %% 4, blocks, reps");
+  hog_kernel<<<blocks, kBlock, 0, (hipStream_t)stream>>>((f4*)dst, (const f4*)src, (long long)n / 4, reps);
+  return check_launch("hog");
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_dyn(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    unsigned long long* counter, int blocks_per_cu, void* stream) {
+  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
+  hipStream_t st = (hipStream_t)stream;
+  CFA_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(*counter), st));
+  mix8_dyn_kernel<<<grid, kBlock, 0, st>>>(out, f, nvec, counter);
+  return check_launch("mix8_dyn");
+}
