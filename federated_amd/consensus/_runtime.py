@@ -541,6 +541,44 @@ class HostMixer:
         kept_n = int(plan.count_host[0]) if compress is not None else None
         return plan.unpack(), kept_n
 
+    def _mewma_tf1_zero_copy(self, layout, W, states, grads, rho, lr1, lr2, split, init, use_filtered, flags,
+                             st) -> List[np.ndarray]:
+        """mewma_tf1 on pinned fp64 rows updated in place by the kernel over PCIe (row 0 = W,
+        rows 1..n = the saved states' slots, rows n+1..2n = the gradients); one launch per run
+        of layers with equal dtype flags; the states are written back into the caller's arrays
+        at their slots. Returns the W arrays (fp64)."""
+        n = len(grads)
+        layout = _layout_of(W) if layout is None else layout
+        plan = self._zc_plan("mewma64", layout, 2 * n, np.float64)
+        rows = plan.rows
+        sizes = layout.sizes
+        plan.pack(W, [])  # row 0 (the remaining rows are filled below)
+        for j in range(n):
+            for k, v in enumerate(plan.views[1 + j]):
+                np.copyto(v, np.asarray(states[k])[..., j].reshape(-1), casting="unsafe")
+            g = grads[j]
+            for k, v in enumerate(plan.views[1 + n + j]):
+                a = np.asarray(g[k])
+                if a.size != sizes[k]:
+                    raise ValueError(f"gradient {j} tensor {k} has {a.size} elements, layout expects {sizes[k]}")
+                np.copyto(v, a.reshape(-1), casting="unsafe")
+        sh = plan.stream_handle(st)
+        ones = plan.strides_one()
+        for k0, k1, f32 in plan.runs(tuple(flags)):
+            b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
+            rc = plan.lib.cfa_mewma_tf1_f64(plan.hb + 8 * b, plan.row_table(1, n, b), plan.row_table(1 + n, n, b),
+                                            ones, n, float(rho), float(lr1), float(lr2), max(0, min(split, e) - b),
+                                            int(bool(init)), int(bool(use_filtered)), int(f32), e - b, sh)
+            _lib.check("cfa_mewma_tf1_f64", rc)
+        _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
+        for j in range(n):
+            for k, v in enumerate(plan.views[1 + j]):
+                states[k][..., j] = v.reshape(layout.shapes[k])
+        P = layout.P
+        flat = rows[0, :P].copy()
+        return [flat[b:e].reshape(shp) for (b, e), shp in
+                zip((layout.segment(k) for k in range(len(sizes))), layout.shapes)]
+
     def fold64(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float], rule: int,
                divisors: Optional[Sequence[float]] = None) -> List[np.ndarray]:
         """fp64 fold (``cfa_fold_f64``) of per-layer arrays widened to fp64 buckets; returns fp64
@@ -594,6 +632,12 @@ class HostMixer:
         if n and any(len({f32(g[k]) for g in grads}) > 1 for k in range(len(W))):
             raise ValueError("neighbour gradients of one layer must share a dtype")
         st_ = self._stream()
+        if TF1_ZERO_COPY and n > 0:
+            W_out = self._mewma_tf1_zero_copy(layout, W, states, grads, rho, lr1, lr2, split, init, use_filtered,
+                                              flags, st_)
+            u32 = lambda k: bool(flags[k] & (TF1_STATE_F32 if use_filtered else TF1_GRAD_F32))
+            return [w.astype(np.float32) if (flags[k] & TF1_W_F32 and u32(k)) and f32(W[k]) else w
+                    for k, w in enumerate(W_out)]
         with torch.cuda.stream(st_):
             dW = self._upload64(layout, W)
             ds = [self._upload64(layout, [np.asarray(st)[..., j] for st in states]) for j in range(n)]
@@ -684,6 +728,22 @@ class _ZeroCopyPlan:
             isz = self.dtype.itemsize
             t = self._tables[b] = _lib.ptr_table([self.hb + isz * (self.pitch * (j + 1) + b)
                                                   for j in range(self.n)])
+        return t
+
+    def row_table(self, first: int, count: int, b: int):
+        """Pointer table of rows first..first+count-1 at element offset ``b`` (cached)."""
+        key = ("rows", first, count, b)
+        t = self._tables.get(key)
+        if t is None:
+            isz = self.dtype.itemsize
+            t = self._tables[key] = _lib.ptr_table([self.hb + isz * (self.pitch * r + b)
+                                                    for r in range(first, first + count)])
+        return t
+
+    def strides_one(self):
+        t = self._tables.get("ones")
+        if t is None:
+            t = self._tables["ones"] = _lib.int64_array([1] * max(1, self.n))
         return t
 
     def pack(self, local, nbrs) -> None:

@@ -34,77 +34,126 @@ def _flat(model) -> np.ndarray:
                            np.asarray(W2, np.float32).reshape(-1), np.asarray(np.squeeze(b2), np.float32).reshape(-1)])
 
 
+class _GradPlan:
+    """Reusable state of one gradient-evaluation shape on one thread: pinned staging (x, y, the
+    M models, the int32 row tables), its device copy, the batch-split workspace and a pinned
+    output that the kernel writes directly (zero-copy), plus the bound launch arguments."""
+
+    def __init__(self, eng, ml_model, shapes, M, x_shape, y_shape, geom):
+        self.eng, self.lib = eng, eng.lib
+        self.shapes = shapes
+        self.sizes = [int(np.prod(sh)) for sh in shapes]
+        self.offs = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
+        P = self.P = int(self.offs[-1])
+        self.M = M
+        nx, ny = int(np.prod(x_shape)), int(np.prod(y_shape))
+        self.nx, self.ny = nx, ny
+        total = self.total = nx + ny + M * P + 2 * M
+        self.host = torch.empty(total, dtype=torch.float32, pin_memory=True)
+        self.out = torch.empty(M * P, dtype=torch.float32, pin_memory=True)
+        self.dev = torch.empty(total, dtype=torch.float32, device=eng.device)
+        B = int(x_shape[0])
+        n_ws = int(self.lib.cfa_ge_grad_workspace_elems(M, B, P))
+        self.ws = torch.empty(max(n_ws, 1), dtype=torch.float32, device=eng.device)
+        hv = self.host.numpy()
+        self.xv, self.yv = hv[:nx].reshape(x_shape), hv[nx:nx + ny].reshape(y_shape)
+        self.mv = hv[nx + ny:nx + ny + M * P].reshape(M, P)
+        self.views = [[self.mv[i, self.offs[k]:self.offs[k + 1]] for k in range(4)] for i in range(M)]
+        rows = hv[nx + ny + M * P:total].view(np.int32)
+        rows[:M] = np.arange(M, dtype=np.int32)
+        rows[M:] = 0
+        d = self.dev.data_ptr()
+        out = eng.host_device_ptr(self.out)
+        xp, yp, mp = d, d + 4 * nx, d + 4 * (nx + ny)
+        rp = d + 4 * (nx + ny + M * P)
+        common = (self.ws.data_ptr(), n_ws, M)
+        if ml_model == 1:
+            self.fn = self.lib.cfa_ge_grad_cnn_rows_f32
+            self.args = (xp, yp, B, int(x_shape[1]), int(y_shape[1]), int(geom["filter"]), int(geom["number"]),
+                         int(geom["stride"]), mp, rp, rp + 4 * M, out) + common
+            self.name = "cfa_ge_grad_cnn_rows_f32"
+        else:
+            self.fn = self.lib.cfa_ge_grad_2nn_rows_f32
+            self.args = (xp, yp, B, int(x_shape[1]), int(geom["intermediate_nodes"]), int(y_shape[1]), mp, rp,
+                         rp + 4 * M, out) + common
+            self.name = "cfa_ge_grad_2nn_rows_f32"
+        self.host_ptr, self.dev_ptr = self.host.data_ptr(), d
+        self._sh = None
+
+    def run(self, x, y, models, st) -> List[list]:
+        np.copyto(self.xv, x, casting="unsafe")  # fp32 rounding, as the tf.float32 placeholders round
+        np.copyto(self.yv, y, casting="unsafe")
+        sizes = self.sizes
+        for i, m in enumerate(models):
+            parts = (m[0], m[1], m[2], m[3])
+            for k in range(4):
+                a = np.asarray(parts[k])
+                if a.size != sizes[k]:
+                    raise ValueError("all models must share the first model's shapes")
+                np.copyto(self.views[i][k], a.reshape(-1), casting="unsafe")
+        if self._sh is None or self._sh[0] is not st:
+            self._sh = (st, int(st.cuda_stream))
+        sh = self._sh[1]
+        lib = self.lib
+        from .. import _lib
+        _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(self.dev_ptr, self.host_ptr, 4 * self.total, sh))
+        _lib.check(self.name, self.fn(*self.args, sh))
+        _lib.check("cfa_stream_synchronize", lib.cfa_stream_synchronize(sh))
+        g = self.out.numpy()[:self.M * self.P].reshape(self.M, self.P).copy()
+        offs, shapes = self.offs, self.shapes
+        return [[g[i, offs[k]:offs[k + 1]].reshape(shapes[k]) for k in range(4)] for i in range(self.M)]
+
+
 def gradients_batched(ml_model: int, x, y, models: Sequence, stride: int = 1, device=None) -> List[list]:
     """Gradients of the device's cost at every model of ``models`` (list of (W1, b1, W2, b2)),
     in ONE kernel launch. x, y and the models are packed into one pinned staging buffer (one
-    H2D); the gradients come back with one D2H. Returns one list of four fp32 arrays per model."""
+    H2D); the kernel writes the gradients straight into pinned host memory. Everything but the
+    pack, the copy, the launch and the unpack is prepared once per shape (``_GradPlan``).
+    Returns one list of four fp32 arrays per model."""
     if not models:
         return []
     from ._runtime import mixer
     hm = mixer() if device is None else None
     eng = hm.engine if hm is not None else get_engine(device)
     W1 = np.asarray(models[0][0])
-    shapes = [W1.shape, (int(np.size(models[0][1])),), np.asarray(models[0][2]).shape, (int(np.size(models[0][3])),)]
-    sizes = [int(np.prod(s)) for s in shapes]
-    P, M = sum(sizes), len(models)
+    shapes = (W1.shape, (int(np.size(models[0][1])),), np.asarray(models[0][2]).shape,
+              (int(np.size(models[0][3])),))
+    M = len(models)
     x = np.asarray(x)
     y = np.asarray(y)
     if x.ndim != 2 or y.ndim != 2 or x.shape[0] != y.shape[0]:
         raise ValueError("x must be [B, inputs] and y [B, classes]")
-    nx, ny = x.size, y.size
-    B = int(x.shape[0])
-    # staging: x, y, the M models, then the int32 row tables of the population-form launch
-    # (evaluation m = model m on the one data set), all in one H2D
-    total = nx + ny + M * P + 2 * M
-    # each evaluation's batch split over several workgroups (partials summed in a fixed order)
-    n_ws = int(eng.lib.cfa_ge_grad_workspace_elems(M, B, P))
+    if ml_model == 1:
+        if W1.ndim != 3 or W1.shape[1] != 1:
+            raise ValueError("CNN W1 must be [filter, 1, number]")
+        geom = {"filter": W1.shape[0], "number": W1.shape[2], "stride": int(stride)}
+    elif ml_model == 2:
+        geom = {"intermediate_nodes": W1.shape[1]}
+    else:
+        raise ValueError("Unable to set the ML model paramters")
+    key = (ml_model, shapes, M, x.shape, y.shape, tuple(sorted(geom.items())))
     if hm is not None:
         st = hm._stream()
-        host = hm._cached("h_grad", total, torch.float32, pinned=True)
-        dbuf = hm._cached("d_grad", total + M * P, torch.float32)
-        h_out = hm._cached("h_grad_out", M * P, torch.float32, pinned=True)
-        ws = hm._cached("d_grad_ws", n_ws, torch.float32) if n_ws else None
+        plans = getattr(hm._tls, "grad_plans", None)
+        if plans is None:
+            plans = hm._tls.grad_plans = {}
     else:
         st = torch.cuda.Stream(eng.device)
-        host = torch.empty(total, dtype=torch.float32, pin_memory=True)
-        dbuf = torch.empty(total + M * P, dtype=torch.float32, device=eng.device)
-        h_out = torch.empty(M * P, dtype=torch.float32, pin_memory=True)
-        ws = torch.empty(n_ws, dtype=torch.float32, device=eng.device) if n_ws else None
-    hv = host.numpy()
-    hv[:nx] = x.reshape(-1)            # fp32 rounding, as the tf.float32 placeholders round
-    hv[nx:nx + ny] = y.reshape(-1)
-    rows = hv[nx + ny + M * P:total].view(np.int32)
-    rows[:M] = np.arange(M, dtype=np.int32)
-    rows[M:] = 0
-    mv = hv[nx + ny:nx + ny + M * P].reshape(M, P)
-    offs = np.concatenate([[0], np.cumsum(sizes)])
-    for i, m in enumerate(models):
-        parts = [np.asarray(m[0]), np.squeeze(m[1]), np.asarray(m[2]), np.squeeze(m[3])]
-        for k in range(4):
-            if np.size(parts[k]) != sizes[k]:
-                raise ValueError("all models must share the first model's shapes")
-            mv[i, offs[k]:offs[k + 1]] = np.asarray(parts[k]).reshape(-1)
-    with torch.cuda.stream(st):
-        dbuf[:total].copy_(host, non_blocking=True)
-        xt = dbuf[:nx].view(x.shape)
-        yt = dbuf[nx:nx + ny].view(y.shape)
-        mt = dbuf[nx + ny:nx + ny + M * P].view(M, P)
-        rt = dbuf[nx + ny + M * P:total].view(torch.int32)
-        gt = dbuf[total:total + M * P].view(M, P)
+        plans = {}
+    plan = plans.get(key)
+    if plan is None:
+        if len(plans) >= 8:
+            plans.pop(next(iter(plans)))
+        P = sum(int(np.prod(sh)) for sh in shapes)
         if ml_model == 1:
-            if W1.ndim != 3 or W1.shape[1] != 1:
-                raise ValueError("CNN W1 must be [filter, 1, number]")
-            geom = {"filter": W1.shape[0], "number": W1.shape[2], "stride": int(stride)}
-        elif ml_model == 2:
-            geom = {"intermediate_nodes": W1.shape[1]}
-        else:
-            raise ValueError("Unable to set the ML model paramters")
-        eng.grad_rows(ml_model, xt.view(1, *x.shape), yt.view(1, *y.shape), mt, rt[:M], rt[M:], gt, geom,
-                      stream=st, workspace=ws)
-        h_out.copy_(dbuf[total:total + M * P], non_blocking=True)
-        st.synchronize()
-        g = h_out.numpy().reshape(M, P).copy()
-    return [[g[i, offs[k]:offs[k + 1]].reshape(shapes[k]) for k in range(4)] for i in range(M)]
+            L2 = -(-(-(-x.shape[1] // stride)) // stride)
+            if P != geom["filter"] * geom["number"] + geom["number"] + L2 * geom["number"] * y.shape[1] + y.shape[1]:
+                raise ValueError("CNN bucket size does not match the geometry")
+        elif P != x.shape[1] * geom["intermediate_nodes"] + geom["intermediate_nodes"] + \
+                geom["intermediate_nodes"] * y.shape[1] + y.shape[1]:
+            raise ValueError("2NN bucket size does not match the geometry")
+        plan = plans[key] = _GradPlan(eng, ml_model, shapes, M, x.shape, y.shape, geom)
+    return plan.run(x, y, models, st)
 
 
 def gradients(ml_model: int, x, y, W1, b1, W2, b2, stride: int = 1, device=None) -> list:

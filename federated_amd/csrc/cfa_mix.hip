@@ -39,6 +39,11 @@ extern "C" int cfa_stream_synchronize(void* stream) {
   CFA_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   return CFA_OK;
 }
+extern "C" int cfa_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes && (!dst || !src)) return fail(CFA_E_INVALID, "null copy pointer");
+  if (bytes) CFA_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream));
+  return CFA_OK;
+}
 extern "C" int cfa_counter_fetch(unsigned long long* counter, unsigned long long* host_dst, void* stream) {
   if (!counter || !host_dst) return fail(CFA_E_INVALID, "null counter or destination");
   hipStream_t st = (hipStream_t)stream;

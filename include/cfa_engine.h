@@ -118,8 +118,11 @@ CFA_API int cfa_device_prepare(int device);
 
 /* Host-path helpers (the per-call drop-in path): hipStreamSynchronize, and a
  * stream-ordered fetch of a device uint64 counter (e.g. a compression kept_count) into host
- * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero. */
+ * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero; and one
+ * asynchronous copy (the pinned staging of a batch of inputs). */
 CFA_API int cfa_stream_synchronize(void* stream);
+/* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream): the staging copy of the host path. */
+CFA_API int cfa_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
 CFA_API int cfa_counter_fetch(unsigned long long* counter, unsigned long long* host_dst, void* stream);
 
 /* ---------------------------------------------------------------------------------------
