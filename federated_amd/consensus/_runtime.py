@@ -391,7 +391,7 @@ class HostMixer:
         ``grads[j]`` (per-layer arrays) and the per-layer saved-state arrays ``states[k]`` of shape
         [..., N] (updated IN PLACE at slot j, as the reference does). ``lrs`` = per-layer learning
         rate; layers with the first rate must precede the others (layer 1 then layer 2)."""
-        layout = BucketLayout.of(W)
+        layout = _layout_of(W)
         n = len(grads)
         first_other = next((k for k in range(len(lrs)) if lrs[k] != lrs[0]), len(lrs))
         if any(lr != lrs[-1] for lr in lrs[first_other:]):
@@ -582,13 +582,24 @@ class HostMixer:
     def fold64(self, local: Sequence, nbrs: Sequence[Sequence], alphas: Sequence[float], rule: int,
                divisors: Optional[Sequence[float]] = None) -> List[np.ndarray]:
         """fp64 fold (``cfa_fold_f64``) of per-layer arrays widened to fp64 buckets; returns fp64
-        arrays with the local shapes. One H2D of all buckets, one launch, one D2H. A neighbour
+        arrays with the local shapes. By default (``TF1_ZERO_COPY``) the kernel reads the pinned
+        rows and writes the pinned output in place; otherwise one H2D of all buckets, one launch,
+        one D2H. A neighbour
         may be given as a callable ``fill(dst)`` that writes its flat fp64 bucket into the pinned
         staging row ``dst`` (the MQTT payload decoder does)."""
-        layout = BucketLayout.of(local)
+        layout = _layout_of(local)
         P, n = layout.P, len(nbrs)
         _check_coefficients(n, alphas, divisors if rule == _lib.RULE_SEQUENTIAL_DIV else None)
         st = self._stream()
+        if TF1_ZERO_COPY:  # the kernel reads the pinned fp64 rows and writes the pinned output in place
+            plan = self._zc_plan("fold64", layout, n, np.float64)
+            plan.pack(local, nbrs)
+            sh = plan.stream_handle(st)
+            div = _lib.double_array([float(x) for x in divisors]) if divisors is not None else None
+            _lib.check("cfa_fold_f64", plan.lib.cfa_fold_f64(plan.ob, plan.hb, plan.table, plan.coeffs(alphas, True),
+                                                             div, n, int(rule), P, sh))
+            _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
+            return plan.unpack()
         with torch.cuda.stream(st):
             host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
             hv = host.numpy().reshape(n + 1, P)
@@ -618,7 +629,7 @@ class HostMixer:
         operation is promoted as numpy 2 promotes it for the arrays' dtypes (Python-float rho and
         learning rates), so the result is the reference's: fp64 model arrays for its fp64
         gradients. ``lrs`` as in ``mewma``."""
-        layout = BucketLayout.of(W)
+        layout = _layout_of(W)
         n = len(grads)
         first_other = next((k for k in range(len(lrs)) if lrs[k] != lrs[0]), len(lrs))
         if any(lr != lrs[-1] for lr in lrs[first_other:]):
@@ -626,10 +637,11 @@ class HostMixer:
         split = int(layout.offsets[first_other])
         lr1, lr2 = float(lrs[0]), float(lrs[-1])
         from ..engine import TF1_GRAD_F32, TF1_STATE_F32, TF1_W_F32
-        f32 = lambda a: np.asarray(a).dtype == np.float32
+        f32 = lambda a: _dtype(a) == _F32
+        gf = [[f32(g[k]) for g in grads] for k in range(len(W))]
         flags = [(TF1_STATE_F32 if f32(states[k]) else 0) | (TF1_W_F32 if f32(W[k]) else 0)
-                 | (TF1_GRAD_F32 if n and all(f32(g[k]) for g in grads) else 0) for k in range(len(W))]
-        if n and any(len({f32(g[k]) for g in grads}) > 1 for k in range(len(W))):
+                 | (TF1_GRAD_F32 if n and all(gf[k]) else 0) for k in range(len(W))]
+        if n and any(len(set(gf[k])) > 1 for k in range(len(W))):
             raise ValueError("neighbour gradients of one layer must share a dtype")
         st_ = self._stream()
         if TF1_ZERO_COPY and n > 0:

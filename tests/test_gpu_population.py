@@ -490,3 +490,55 @@ def test_rccl_reduce_sum_world1(gpu):
         assert torch.equal(x, ref)
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("rule", [0, 2, 3])
+@pytest.mark.parametrize("n,P_odd", [(3, False), (2, True), (17, True)])
+def test_fold64_zero_copy_equals_staged(gpu, monkeypatch, rule, n, P_odd):
+    """HostMixer.fold64 (the fp64 server-side folds: MQTT PS_server, CFA_FA) on pinned rows in
+    place equals the staged H2D / D2H path bit for bit, for every fp64 rule, a payload filler
+    neighbour, odd P and fan-in above CFA_MAX_FANIN."""
+    from federated_amd import _lib
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(rule * 10 + n)
+    shapes = [(5, 7) if P_odd else (4, 8), (3,) if P_odd else (4,)]
+    local = [rng.standard_normal(s) for s in shapes]
+    nbrs = [[rng.standard_normal(s) for s in shapes] for _ in range(n)]
+    flat = np.concatenate([a.reshape(-1) for a in nbrs[-1]])
+    nbrs[-1] = lambda dst: np.copyto(dst, flat)  # a payload decoder writes its row itself
+    al = [0.9] * n
+    div = [float(n)] * n if rule == _lib.RULE_SEQUENTIAL_DIV else None
+    mx = R.mixer()
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", False)
+    ref = mx.fold64(local, nbrs, al, rule, div)
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", True)
+    got = mx.fold64(local, nbrs, al, rule, div)
+    for a, r in zip(got, ref):
+        assert a.dtype == np.float64 and np.array_equal(a, r)
+
+
+@pytest.mark.parametrize("use_filtered,init", [(True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("state_dt,grad_dt", [(np.float64, np.float64), (np.float32, np.float32),
+                                              (np.float64, np.float32)])
+def test_mewma_tf1_zero_copy_equals_staged(gpu, monkeypatch, use_filtered, init, state_dt, grad_dt):
+    """HostMixer.mewma_tf1 (CFA-GE) on pinned rows updated in place equals the staged path bit
+    for bit: the returned model, and the caller's saved-state arrays at their slots."""
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(7)
+    shapes = [(16, 1, 8), (8,), (168, 8), (8,)]
+    N, n = 3, 2
+    W = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    grads = [[rng.standard_normal(s).astype(grad_dt) for s in shapes] for _ in range(n)]
+    st0 = [rng.standard_normal(s + (N,)).astype(state_dt) for s in shapes]
+    mx = R.mixer()
+    lrs = (0.1, 0.1, 0.2, 0.2)
+    s_ref = [x.copy() for x in st0]
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", False)
+    ref = mx.mewma_tf1(W, s_ref, grads, 0.99, lrs, init, use_filtered)
+    s_got = [x.copy() for x in st0]
+    monkeypatch.setattr(R, "TF1_ZERO_COPY", True)
+    got = mx.mewma_tf1(W, s_got, grads, 0.99, lrs, init, use_filtered)
+    for a, r in zip(got, ref):
+        assert a.dtype == r.dtype and np.array_equal(a, r)
+    for a, r in zip(s_got, s_ref):
+        assert a.dtype == r.dtype and np.array_equal(a, r)
