@@ -564,11 +564,11 @@ class HostMixer:
                 np.copyto(v, a.reshape(-1), casting="unsafe")
         sh = plan.stream_handle(st)
         ones = plan.strides_one()
-        for k0, k1, f32 in plan.runs(tuple(flags)):
+        for k0, k1, mask in plan.runs(tuple(flags)):
             b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
             rc = plan.lib.cfa_mewma_tf1_f64(plan.hb + 8 * b, plan.row_table(1, n, b), plan.row_table(1 + n, n, b),
                                             ones, n, float(rho), float(lr1), float(lr2), max(0, min(split, e) - b),
-                                            int(bool(init)), int(bool(use_filtered)), int(f32), e - b, sh)
+                                            int(bool(init)), int(bool(use_filtered)), int(mask), e - b, sh)
             _lib.check("cfa_mewma_tf1_f64", rc)
         _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
         for j in range(n):
@@ -654,10 +654,10 @@ class HostMixer:
             dW = self._upload64(layout, W)
             ds = [self._upload64(layout, [np.asarray(st)[..., j] for st in states]) for j in range(n)]
             dg = [self._upload64(layout, g) for g in grads]
-            for k0, k1, f32 in self._runs(flags):
+            for k0, k1, mask in self._runs(flags):
                 b, e = layout.segment(k0)[0], layout.segment(k1 - 1)[1]
                 self.engine.mewma_tf1_f64(dW[b:e], [x[b:e] for x in ds], [x[b:e] for x in dg], rho, lr1, lr2,
-                                          max(0, min(split, e) - b), init, use_filtered, f32, stream=st_)
+                                          max(0, min(split, e) - b), init, use_filtered, mask, stream=st_)
             W_out = dW.cpu().numpy()
             s_out = [x.cpu().numpy() for x in ds]
         for j in range(n):
