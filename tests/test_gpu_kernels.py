@@ -564,3 +564,31 @@ def test_tf1_wide_equals_f64_rows(gpu, n, P, off, mode):
     torch.cuda.synchronize()
     assert torch.equal(out_w, out_f)
     assert int(kw.item()) == int(kf.item())
+
+
+def test_full_size_tf1_wide_and_sharded_fedavg(gpu):
+    """BASELINE size (8 neighbours x 25M): the TF1 wide kernel against the oracle's fp64 chain
+    over the whole bucket, bit for bit (fp32 arrays in, the reference's fp64 result out), and
+    the sharded-FedAvg closed form (cfa_mix_f32 over 8 models + the global one) within 1e-5
+    normwise of the sequential FedAvg fold."""
+    from federated_amd import _lib
+    from federated_amd.ps_shard import ShardedFedAvg
+    P, n = 25_000_000, 8
+    g = torch.Generator(device="cuda").manual_seed(20261016)
+    rows = torch.randn(n + 1, P, generator=g, device="cuda")
+    al = [0.5 / (n + 1)] * n
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    _lib.call("cfa_mix_tf1_wide_f32", out.data_ptr(), rows[0].data_ptr(),
+              _lib.ptr_table([rows[j].data_ptr() for j in range(1, n + 1)]), _lib.double_array(al), n, P, 0, 0, 0,
+              None, gpu.stream_handle())
+    h = rows.cpu().numpy()
+    ref = O.tf1_mix_flat(h[0], [h[j] for j in range(1, n + 1)], al)
+    torch.cuda.synchronize()
+    assert ref.dtype == np.float64 and np.array_equal(out.cpu().numpy(), ref)
+    del out
+    ps = ShardedFedAvg(0, 1, n, P, "cuda", None, gpu, update_factor=1.0)
+    ps.models.copy_(rows[1:])
+    ps.params.copy_(rows[0])
+    got = ps.aggregate().cpu().numpy()
+    ref = O.ps_fedavg([h[0]], [[h[j]] for j in range(1, n + 1)], 1.0)[0]
+    assert np.max(np.abs(got - ref)) <= 1e-5 * np.max(np.abs(ref))

@@ -55,7 +55,7 @@ al = [0.5, 0.5]
 res["C1"] = {
     "P": P, "n": 2,
     "mix_tf1_us": med(lambda: mx.mix_tf1(local, nbrs, al)),
-    "numpy_tf1_us": med(lambda: O.tf1_mix(local, nbrs, 1.0, al)),
+    "numpy_tf1_us": med(lambda: O.tf1_mix(local, nbrs, 1.0, [np.float64(a) for a in al])),
     "mix_fp32_us": med(lambda: mx.mix(local, nbrs, al)),
     "numpy_fp32_us": med(lambda: [O.sequential_mix(local[k], [x[k] for x in nbrs], al) for k in range(4)]),
 }
@@ -68,7 +68,7 @@ al2 = [0.25, 0.25, 0.25]
 
 
 def numpy_c2():
-    out = O.tf1_mix(local2, nbrs2, 1.0, al2)
+    out = O.tf1_mix(local2, nbrs2, 1.0, [np.float64(a) for a in al2])
     O.tf1_compress(np.asarray(out[2], dtype=np.float64), local2[2], 2)
 
 

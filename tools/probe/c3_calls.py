@@ -40,7 +40,7 @@ grads = [mk(np.float64), mk(np.float64)]
 mx = R.mixer()
 res = {"experiment": "tools/probe/c3_calls.py", "P": 1488, "n": 2}
 res["stage1_mix_tf1_us"] = med(lambda: mx.mix_tf1(local, nbrs, [0.5, 0.5]))
-res["numpy_stage1_us"] = med(lambda: O.tf1_mix(local, nbrs, 1.0, [0.5, 0.5]))
+res["numpy_stage1_us"] = med(lambda: O.tf1_mix(local, nbrs, 1.0, [np.float64(0.5)] * 2))
 res["gradients_batched_us"] = med(lambda: _tf1_models.gradients_batched(1, x, y, nbrs, stride=5))
 res["numpy_gradients_us"] = med(lambda: [O.tf1_cnn_grads(x, y, *m, 5) for m in nbrs], 30)
 res["mewma_tf1_us"] = med(lambda: mx.mewma_tf1(local, states, grads, 0.99, (0.1, 0.1, 0.2, 0.2), False, True))
