@@ -132,14 +132,14 @@ def _seeded(g, P):
     return torch.randn(P, generator=torch.Generator().manual_seed(7000 + g))
 
 
-def _worker(rank, world, port, D, h, P, partition, gd, relay, staged, q):
+def _worker(rank, world, port, D, h, P, partition, gd, relay, staged, q, hr=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from federated_amd.dist import TorchTransport
         from oracle.cfa_oracle import sequential_mix
-        shard, info = make_ring_shard(rank, world, D, h, h, P, "cpu", TorchTransport(), None,
+        shard, info = make_ring_shard(rank, world, D, h, h if hr is None else hr, P, "cpu", TorchTransport(), None,
                                       partition=partition, dev_groups=gd, relay=relay, staged=staged)
         lo, hi = info["slice"]
         plan = shard.plan
@@ -191,6 +191,27 @@ def test_routed_exchange_gloo(world, D, partition, gd, relay, staged):
         res[r] = ok
         if partition == "devices" and world == 8 and relay:
             assert used_relay
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
+def test_v4_ring_c5_shape_gloo():
+    """Config 5's topology sharded as the driver's 8-GPU run would shard it: 128 devices on the
+    TF2 v4 ring (N < 2: in-neighbour ii-1 only, consensus_v4.py:133-137, hl = 1, hr = 0) over 8
+    ranks, routed exchange, every device's mix equal to the unsharded oracle's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, D, P = 8, 128, 515
+    port = 32500 + (os.getpid() % 997)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, D, 1, P, "devices", None, True, True, q, 0))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, ok, _ = q.get(timeout=180)
+        res[r] = ok
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
