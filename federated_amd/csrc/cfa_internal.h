@@ -255,6 +255,31 @@ __device__ __forceinline__ void block_add_count(unsigned kept, unsigned long lon
 constexpr long long kMaxChunkVec = 1LL << 27;
 constexpr int kStoreSc1 = 16;
 
+// Streaming store of one 16-byte vector with the sc1 write-through policy, as the headline mix
+// stores its output (kStoreSc1): through a buffer resource when every byte offset of the output
+// fits the 31 bits the kernels pass, else a nontemporal global store. The choice is uniform per
+// launch (one scalar branch).
+struct Sc1Out {
+  __amdgpu_buffer_rsrc_t r;
+  void* base;
+  bool buf;
+};
+__device__ __forceinline__ Sc1Out sc1_out(void* base, long long bytes) {
+  Sc1Out o;
+  o.base = base;
+  o.buf = bytes <= 0x7FFFFFF0LL;
+  o.r = __builtin_amdgcn_make_buffer_rsrc(base, 0, o.buf ? (unsigned)bytes : 0u, 0x00020000);
+  return o;
+}
+template <typename V>
+__device__ __forceinline__ void st16_sc1(const Sc1Out& o, long long idx, V v) {  // idx: 16-byte units
+  static_assert(sizeof(V) == 16, "16-byte vectors only");
+  if (o.buf)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), o.r, (int)(idx * 16), 0, kStoreSc1);
+  else
+    __builtin_nontemporal_store(v, reinterpret_cast<V*>(o.base) + idx);
+}
+
 // fp64 form of the epilogue for the fp64 chains (TF1 W_up_l2 is fp64 in the reference).
 __device__ __forceinline__ double compress_one_d(double y, double ref, const CompressParams& cp,
                                                  unsigned& kept) {

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fa
                                                                    CompressParams cp) {
   constexpr int U = (N + 1) * 4 <= 40 ? 4 : ((N + 1) * 2 <= 40 ? 2 : 1);
   constexpr long long kTile = (long long)kBlock * U;
+  const Sc1Out o = sc1_out(out, nvec * 16);
   unsigned kept = 0;
   for (long long base = (long long)blockIdx.x * kTile + threadIdx.x; base < nvec;
        base += (long long)gridDim.x * kTile) {
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fa
           if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
         }
       }
-      st4<true>(out, i, w);
+      st16_sc1(o, i, w);
     }
   }
   block_add_count(kept, cp.kept);
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float*
       if (i >= nvec) continue;
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
-      st4<true>(y, i, v[u]);
+      st4<true>(y, i, v[u]);  // in place: an sc1 store measured 20% slower here
     }
   }
   for (long long i = 4 * nvec + (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += stride) {

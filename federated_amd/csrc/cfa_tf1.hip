@@ -17,6 +17,8 @@ namespace {
 // chain passes through an fp64 scratch bucket (FROM64 / kOutScratch64); cfa_mix_tf1_wide_f32
 // writes the unrounded fp64 result instead (and chains its passes in that output).
 // ------------------------------------------------------------------------------------------
+typedef double d2 __attribute__((ext_vector_type(2)));
+
 struct Tf1Fanin {
   const float* local;               // pre-mix local: step-0 input and DPCM reference
   const double* w64;                // running fp64 w of the previous pass (FROM64)
@@ -32,6 +34,7 @@ template <int N, bool FROM64, int OUT>
 __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin f, long long nvec,
                                                               CompressParams cp, int compress) {
   unsigned kept = 0;
+  const Sc1Out o = sc1_out(out, nvec * 16);  // used by the fp32 output only
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
        i += (long long)gridDim.x * kBlock) {
     f4 x[N];
@@ -62,11 +65,11 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin
     }
     if constexpr (OUT == kOutF32) {
       const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
-      st4<true>(reinterpret_cast<float*>(out), i, y);
-    } else {
-      double* o = reinterpret_cast<double*>(out) + 4 * i;
+      st16_sc1(o, i, y);
+    } else {  // fp64 out: plain stores (two sc1 halves per lane measured 17% slower)
+      double* od = reinterpret_cast<double*>(out) + 4 * i;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) o[c] = w[c];
+      for (int c = 0; c < 4; ++c) od[c] = w[c];
     }
   }
   if (OUT != kOutScratch64 && compress) block_add_count(kept, cp.kept);
@@ -156,7 +159,6 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fan
 // Vector form of mix_tf1_f64_kernel for 16-byte-aligned buckets: each lane moves two doubles per
 // bucket per vector, U vectors per tile, every load of a tile issued before its first use, the
 // fan-in N and the rule at compile time (the runtime loop above serialises its loads).
-typedef double d2 __attribute__((ext_vector_type(2)));
 template <int N, int RULE, bool STEP0F32>
 __global__ __launch_bounds__(kBlock) void fold_f64_vec_kernel(double* out, F64Fanin f, long long nvec2,
                                                                const double* ref, CompressParams cp,
