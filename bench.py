@@ -64,6 +64,8 @@ def parse():
                    help="whole halo in one exchange step (boundary devices wait for all of it)")
     p.add_argument("--no-params-leg", action="store_true",
                    help="N > 1: skip the second, --partition params measurement")
+    p.add_argument("--no-weak-leg", action="store_true",
+                   help="N > 1: skip the weak-scaling reference leg (--devices devices per GPU)")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
     p.add_argument("--allow-fallback", action="store_true",
                    help="if the requested transport cannot open, fall back to torch.distributed "
@@ -395,8 +397,9 @@ def main():
             dist.destroy_process_group()
             sys.exit(3)
 
-    def build(partition):
-        shard, info = make_ring_shard(rank, world, D, K // 2, K // 2, P, torch.device("cuda", device), transport,
+    def build(partition, devices=None):
+        shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
+                                      transport,
                                       eng, partition=partition, dev_groups=args.device_groups,
                                       relay=not args.no_relay, staged=not args.no_stages,
                                       window_batch=args.window_batch)
@@ -440,6 +443,17 @@ def main():
                 leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
             legs[part if groups is None else f"{part}{groups}"] = leg
             del xshard
+            torch.cuda.empty_cache()
+        if not args.no_weak_leg and not weak:
+            # weak form for reference: the single-GPU population on every rank (D = 128 N), the
+            # same routed halo now hidden under 120 interior mixes per rank
+            Dw = args.devices * world
+            wshard, winfo = build("devices", Dw)
+            wel, _, _ = run_leg(args, wshard, world, args.steps, args.warmup, timed_kernel=False)
+            legs["weak"] = {"value": round(Dw * (K + 2) * P * 4 * args.steps / wel / 1e9, 2),
+                            "ms_per_step": round(wel / args.steps * 1e3, 4), "devices_total": Dw,
+                            "note": f"{args.devices} devices per GPU (population grown with N), devices partition"}
+            del wshard
             torch.cuda.empty_cache()
 
     result = None

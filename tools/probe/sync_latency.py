@@ -21,6 +21,16 @@ for path in _lib.loaded_hip_runtimes():
     hip = ctypes.CDLL(path)
 hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
 hip.hipStreamQuery.restype = ctypes.c_int
+for fn in ("hipEventRecord", "hipEventSynchronize", "hipEventQuery"):
+    getattr(hip, fn).restype = ctypes.c_int
+hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+hip.hipEventQuery.argtypes = [ctypes.c_void_p]
+hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+hip.hipEventCreateWithFlags.restype = ctypes.c_int
+ev_default, ev_nt = ctypes.c_void_p(), ctypes.c_void_p()
+assert hip.hipEventCreateWithFlags(ctypes.byref(ev_default), 0) == 0
+assert hip.hipEventCreateWithFlags(ctypes.byref(ev_nt), 2) == 0  # hipEventDisableTiming
 
 
 def med(fn, n=500):
@@ -79,4 +89,21 @@ res["zc_launch_spin_us"] = med(lambda: (zc_launch(), spin()))
 res["dev_launch_block_us"] = med(lambda: (dev_go(), block()))
 res["dev_launch_spin_us"] = med(lambda: (dev_go(), spin()))
 res["query_idle_us"] = med(lambda: hip.hipStreamQuery(sh))
+
+
+def ev_sync(ev):
+    hip.hipEventRecord(ev, sh)
+    hip.hipEventSynchronize(ev)
+
+
+def ev_spin(ev):
+    hip.hipEventRecord(ev, sh)
+    while hip.hipEventQuery(ev) != 0:
+        pass
+
+
+res["zc_launch_event_sync_us"] = med(lambda: (zc_launch(), ev_sync(ev_default)))
+res["zc_launch_event_nt_sync_us"] = med(lambda: (zc_launch(), ev_sync(ev_nt)))
+res["zc_launch_event_spin_us"] = med(lambda: (zc_launch(), ev_spin(ev_nt)))
+res["zc_launch_block_again_us"] = med(lambda: (zc_launch(), block()))
 print(json.dumps(res))
