@@ -1,0 +1,59 @@
+"""CPU tests of bench.py's host logic that needs no GPU: the live PMC traffic reader (against a
+stand-in `rocprofv3` that writes the counter CSV rocprofv3 writes) and its fallbacks."""
+import os
+import stat
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FAKE = r'''#!/usr/bin/env python3
+import os, sys
+args = sys.argv[1:]
+d = args[args.index("-d") + 1]
+counter = args[args.index("--pmc") + 1]
+if os.environ.get("FAKE_ROCPROF_FAIL"):
+    sys.exit(3)
+os.makedirs(os.path.join(d, "host", "1234"), exist_ok=True)
+val = {"FETCH_SIZE": 439498.625, "WRITE_SIZE": 97656.25}[counter]
+with open(os.path.join(d, "host", "1234", "pmc_counter_collection.csv"), "w") as fh:
+    fh.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
+    for i in range(6):
+        name = '"void (anonymous namespace)::mix_vec_kernel<8, 0, 4, true>(float*)"'
+        fh.write(f"{i},{name},{counter},{val / 2}\n")
+        fh.write(f"{i},{name},{counter},{val / 2}\n")  # per-XCD rows of one dispatch
+        fh.write(f'{100 + i},"void other_kernel()",{counter},1.0\n')
+'''
+
+
+@pytest.fixture
+def fake_rocprof(tmp_path, monkeypatch):
+    exe = tmp_path / "rocprofv3"
+    exe.write_text(FAKE)
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+    monkeypatch.setenv("PATH", f"{tmp_path}{os.pathsep}{os.environ['PATH']}")
+    return exe
+
+
+def test_live_traffic_reads_and_corrects_the_pmc_passes(fake_rocprof):
+    import bench
+    val, note = bench.live_traffic(25_000_000, 8, timeout=60)
+    # read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB; rows of one dispatch summed
+    assert val == pytest.approx(2 * 439498.625 * 1024 + 97656.25 * 1024)
+    assert "this run" in note
+
+
+def test_live_traffic_reports_a_failed_pass(fake_rocprof, monkeypatch):
+    import bench
+    monkeypatch.setenv("FAKE_ROCPROF_FAIL", "1")
+    val, note = bench.live_traffic(25_000_000, 8, timeout=60)
+    assert val is None and "failed" in note
+
+
+def test_live_traffic_without_profiler(monkeypatch, tmp_path):
+    import bench
+    monkeypatch.setenv("PATH", str(tmp_path))
+    val, note = bench.live_traffic(25_000_000, 8, timeout=60)
+    assert val is None and "not on PATH" in note
