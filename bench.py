@@ -64,6 +64,9 @@ def parse():
                    help="whole halo in one exchange step (boundary devices wait for all of it)")
     p.add_argument("--no-params-leg", action="store_true",
                    help="N > 1: skip the second, --partition params measurement")
+    p.add_argument("--no-autotune", action="store_true",
+                   help="N > 1: time the relayed route as planned, without first comparing it with "
+                        "the direct-only route")
     p.add_argument("--no-weak-leg", action="store_true",
                    help="N > 1: skip the weak-scaling reference leg (--devices devices per GPU)")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
@@ -397,12 +400,12 @@ def main():
             dist.destroy_process_group()
             sys.exit(3)
 
-    def build(partition, devices=None):
+    def build(partition, devices=None, relay=None):
         shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
                                       transport,
                                       eng, partition=partition, dev_groups=args.device_groups,
-                                      relay=not args.no_relay, staged=not args.no_stages,
-                                      window_batch=args.window_batch)
+                                      relay=(not args.no_relay) if relay is None else relay,
+                                      staged=not args.no_stages, window_batch=args.window_batch)
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -413,6 +416,24 @@ def main():
         return shard, info
 
     shard, info = build(args.partition)
+    autotune = None
+    if world > 1 and info.get("route", {}).get("relay") and not args.no_autotune:
+        # route autotune, before the timed region: the relayed plan against the direct-only plan,
+        # a few rounds each after warm-up, max over ranks; the faster one is the one timed (the
+        # cost model assumes every link runs at the same rate; this checks it on the node)
+        tune_steps = 3
+        t_rel, _, _ = run_leg(args, shard, world, tune_steps, args.warmup, timed_kernel=False)
+        dshard, dinfo = build(args.partition, relay=False)
+        t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
+        autotune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
+                    "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
+        if t_dir < t_rel:  # same decision on every rank: both times are maxima over ranks
+            shard, info = dshard, dinfo
+            autotune["chosen"] = "direct"
+        else:
+            del dshard
+            autotune["chosen"] = "relayed"
+        torch.cuda.empty_cache()
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
@@ -495,7 +516,8 @@ def main():
                 "halo_route": ({k: route[k] for k in ("relay", "stages", "groups", "messages",
                                                      "max_messages_per_rank_group")}
                                | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
-                                  "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1)}) if route else None,
+                                  "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
+                                  "autotune": autotune}) if route else None,
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
                 "parallelism": f"population-{info['partition']}{world}",
             },
