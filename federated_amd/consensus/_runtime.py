@@ -223,7 +223,8 @@ class HostMixer:
         if plan is None or plan.layout is not layout:
             if len(plans) >= 16:  # bounded: drop the oldest layout
                 plans.pop(next(iter(plans)))
-            plan = plans[key] = _ZeroCopyPlan(self, layout, n, dtype, out_dtype)
+            plan = plans[key] = _ZeroCopyPlan(self, layout, n, dtype, out_dtype,
+                                              counter=kind not in ("mewma64", "fold64"))
         return plan
 
     def _mix_zero_copy(self, layout: BucketLayout, local, nbrs, alphas, divisors, st,
@@ -678,7 +679,8 @@ class _ZeroCopyPlan:
     so a pack is one ``np.copyto`` per layer, with the same dtype conversion as
     ``BucketLayout.pack``."""
 
-    def __init__(self, mixer: "HostMixer", layout: BucketLayout, n: int, dtype, out_dtype=None):
+    def __init__(self, mixer: "HostMixer", layout: BucketLayout, n: int, dtype, out_dtype=None,
+                 counter: bool = True):
         self.layout = layout
         shapes = layout.shapes
         self.P, self.n = self.layout.P, n
@@ -704,12 +706,15 @@ class _ZeroCopyPlan:
         self._runs = {}
         self._sh = None
         # compression count: a device counter (kernel atomics), read back by one 8-byte copy
-        # into a pinned word and re-zeroed in the same stream order (cfa_counter_fetch)
-        self.counter_t = torch.zeros(1, dtype=torch.int64, device=eng.device)
-        torch.cuda.synchronize(eng.device)
-        self.counter = self.counter_t.data_ptr()
-        self.count_pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-        self.count_host = self.count_pinned.numpy()
+        # into a pinned word and re-zeroed in the same stream order (cfa_counter_fetch). Only
+        # the plans whose kernels take an epilogue get one; it is zeroed once, synchronously.
+        self.counter_t = self.counter = self.count_pinned = self.count_host = None
+        if counter:
+            self.counter_t = torch.zeros(1, dtype=torch.int64, device=eng.device)
+            torch.cuda.current_stream(eng.device).synchronize()
+            self.counter = self.counter_t.data_ptr()
+            self.count_pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self.count_host = self.count_pinned.numpy()
 
     def stream_handle(self, st) -> int:
         if self._sh is None or self._sh[0] is not st:
