@@ -533,8 +533,10 @@ class HostMixer:
             rc = plan.lib.cfa_mix_tf1_f64(plan.ob + 8 * b, plan.hb + 8 * b, plan.run_table(b), coeffs, n,
                                           int(bool(f32)), e - b, mode if hit else 0, lo - b if hit else 0,
                                           hi - b if hit else 0, plan.counter if hit else None, sh)
-            if rc != _lib.CFA_OK and compress is not None:
-                plan.reset_count()
+            if rc != _lib.CFA_OK:
+                plan.lib.cfa_stream_synchronize(sh)  # earlier runs may still read the pinned rows
+                if compress is not None:
+                    plan.reset_count()
             _lib.check("cfa_mix_tf1_f64", rc)
         if compress is not None:
             plan.fetch_count(sh)
@@ -570,6 +572,8 @@ class HostMixer:
             rc = plan.lib.cfa_mewma_tf1_f64(plan.hb + 8 * b, plan.row_table(1, n, b), plan.row_table(1 + n, n, b),
                                             ones, n, float(rho), float(lr1), float(lr2), max(0, min(split, e) - b),
                                             int(bool(init)), int(bool(use_filtered)), int(mask), e - b, sh)
+            if rc != _lib.CFA_OK:
+                plan.lib.cfa_stream_synchronize(sh)  # earlier runs may still update the pinned rows
             _lib.check("cfa_mewma_tf1_f64", rc)
         _lib.check("cfa_stream_synchronize", plan.lib.cfa_stream_synchronize(sh))
         for j in range(n):
