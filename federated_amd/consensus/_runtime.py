@@ -93,7 +93,7 @@ def _dtype(a):
 def _layout_of(arrays) -> BucketLayout:
     """BucketLayout of the arrays' shapes, cached per shape tuple (building one costs tens of
     microseconds of numpy calls, which a per-call drop-in path cannot afford)."""
-    key = tuple(np.shape(a) for a in arrays)
+    key = tuple([a.shape if type(a) is np.ndarray else np.shape(a) for a in arrays])
     lay = _layouts.get(key)
     if lay is None:
         if len(_layouts) >= 64:
@@ -443,13 +443,15 @@ class HostMixer:
         _check_coefficients(n, alphas)
         layout = _layout_of(local)
         P = layout.P
+        st = self._stream()
+        if TF1_ZERO_COPY:  # fp32 arrays (what TF hands the drivers) take one wide launch
+            res = self._mix_tf1_wide(layout, local, nbrs, alphas, compress, st)
+            if res is not None:
+                return res
         first = nbrs[0]
         flags = tuple(_dtype(local[k]) == _F32 and not callable(first) and _dtype(first[k]) == _F32
                       for k in range(len(local)))
-        st = self._stream()
         if TF1_ZERO_COPY:
-            if all(flags) and all(not callable(x) and all(_dtype(a) == _F32 for a in x) for x in nbrs[1:]):
-                return self._mix_tf1_wide(layout, local, nbrs, alphas, compress, st)
             return self._mix_tf1_zero_copy(layout, local, nbrs, alphas, compress, flags, st)
         with torch.cuda.stream(st):
             host = self._cached("h_in64", (n + 1) * P, torch.float64, pinned=True)
@@ -491,11 +493,13 @@ class HostMixer:
     def _mix_tf1_wide(self, layout, local, nbrs, alphas, compress, st):
         """mix_tf1 when every array is fp32 (what TF hands the TF1 drivers): fp32 pinned rows, one
         cfa_mix_tf1_wide_f32 launch writing the unrounded fp64 result into a pinned fp64 row.
+        Returns None, launching nothing, when the pack meets an array that is not fp32.
         The same values as the fp64-row path (fp32 values widen exactly; step 0 is the fp32
         subtraction there too) at half the packed and PCIe-read bytes."""
         n = len(nbrs)
         plan = self._zc_plan("tf1w", layout, n, np.float32, out_dtype=np.float64)
-        plan.pack(local, nbrs)
+        if not plan.pack(local, nbrs, require=_F32):
+            return None  # some array is not fp32 (or a filler): the fp64-row path takes it
         sh = plan.stream_handle(st)
         mode, cb, ce = 0, 0, 0
         if compress is not None:
@@ -698,6 +702,7 @@ class _ZeroCopyPlan:
         self.rows = hv
         segs = [self.layout.segment(k) for k in range(len(shapes))]
         self.views = [[hv[m, b:e] for b, e in segs] for m in range(n + 1)]
+        self.shaped_views = [[v.reshape(shp) for v, shp in zip(row, self.layout.shapes)] for row in self.views]
         self.out_np = self.out.numpy()[:self.P]
         self.out_slices = [(slice(b, e), shp) for (b, e), shp in zip(segs, self.layout.shapes)]
         eng = mixer.engine
@@ -767,19 +772,32 @@ class _ZeroCopyPlan:
             t = self._tables["ones"] = _lib.int64_array([1] * max(1, self.n))
         return t
 
-    def pack(self, local, nbrs) -> None:
-        sizes = self.layout.sizes
-        for m, model in enumerate([local] + list(nbrs)):
+    def pack(self, local, nbrs, require=None) -> bool:
+        """Copy every model into its row (converting dtypes). With ``require`` (a dtype), stop and
+        return False at the first array of another dtype or at a filler; True when packed."""
+        sizes, shapes = self.layout.sizes, self.layout.shapes
+        shaped = self.shaped_views
+        for m, model in enumerate((local, *nbrs)):
             if callable(model):  # a filler writes the flat bucket itself (e.g. a payload decoder)
+                if require is not None:
+                    return False
                 model(self.rows[m, :self.P])
                 continue
             if len(model) != len(sizes):
                 raise ValueError(f"expected {len(sizes)} tensors, got {len(model)}")
-            for k, (v, a) in enumerate(zip(self.views[m], model)):
+            for k, a in enumerate(model):
+                if type(a) is np.ndarray and a.shape == shapes[k]:  # the common case: no reshape
+                    if require is not None and a.dtype != require:
+                        return False
+                    np.copyto(shaped[m][k], a, casting="unsafe")
+                    continue
                 a = np.asarray(a)
+                if require is not None and a.dtype != require:
+                    return False
                 if a.size != sizes[k]:
                     raise ValueError(f"tensor {k} has {a.size} elements, layout expects {sizes[k]}")
-                np.copyto(v, a.reshape(-1), casting="unsafe")
+                np.copyto(self.views[m][k], a.reshape(-1), casting="unsafe")
+        return True
 
     def fetch_count(self, sh: int) -> None:
         """Stream-ordered: the device counter's value into ``count_host`` and the counter reset
