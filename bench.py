@@ -519,6 +519,7 @@ def main():
                                   "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
                                   "autotune": autotune}) if route else None,
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
+                "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
             },
             "roofline": {
@@ -568,6 +569,18 @@ def main():
         transport.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def rccl_version():
+    """ncclGetVersion of the RCCL libcfa runs on (e.g. 22703 = 2.27.3), or None."""
+    import ctypes
+    from federated_amd import _lib
+    v = ctypes.c_int(0)
+    try:
+        _lib.call("cfa_rccl_version", ctypes.byref(v))
+    except Exception:
+        return None
+    return int(v.value)
 
 
 def shard_P(info, P):

@@ -103,6 +103,7 @@ SIGNATURES = {
                                             _c_void_p, _c_int, ctypes.c_double, ctypes.c_float, ctypes.c_float,
                                             _c_size_t, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_int, _c_int,
                                             _c_void_p]),
+    "cfa_rccl_version": (_c_int, [_c_int_p]),
     "cfa_comm_unique_id": (_c_int, [_c_void_p]),
     "cfa_comm_init": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_void_p, _c_int]),
     "cfa_comm_destroy": (_c_int, [_c_void_p]),

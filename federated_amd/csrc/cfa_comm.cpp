@@ -42,6 +42,12 @@ static int comm_fail(int code, const char* fmt, ...) {
 
 static_assert(sizeof(ncclUniqueId) == CFA_UNIQUE_ID_BYTES, "unique id size");
 
+extern "C" int cfa_rccl_version(int* version) {
+  if (!version) return comm_fail(CFA_E_INVALID, "null version");
+  CFA_NCCL_CHECK(ncclGetVersion(version));
+  return CFA_OK;
+}
+
 extern "C" int cfa_comm_unique_id(void* id) {
   if (!id) return comm_fail(CFA_E_INVALID, "null unique-id buffer");
   ncclUniqueId uid;

@@ -398,6 +398,8 @@ CFA_API int cfa_ge_population_step_f32(float* const* out_ptrs, const float* cons
 #define CFA_UNIQUE_ID_BYTES 128
 
 /* Fill `id` (CFA_UNIQUE_ID_BYTES bytes) on one rank; share it with the others out of band. */
+/* The RCCL library version libcfa runs on (ncclGetVersion), for the record of a multi-GPU run. */
+CFA_API int cfa_rccl_version(int* version);
 CFA_API int cfa_comm_unique_id(void* id);
 /* Create a communicator for `rank` of `nranks` on HIP device `device`. */
 CFA_API int cfa_comm_init(void** comm, int rank, int nranks, const void* id, int device);
