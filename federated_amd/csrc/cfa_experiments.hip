@@ -409,3 +409,56 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_dyn(
   mix8_dyn_kernel<<<grid, kBlock, 0, st>>>(out, f, nvec, counter);
   return check_launch("mix8_dyn");
 }
+
+// ------------------------------------------------------------------------------------------
+// Standalone compression epilogue variants (tools/probe/compress_sweep.py): U float4 of y and
+// ref per lane, nontemporal or default loads / stores, workgroups per CU.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void compress_x_kernel(float* y, const float* ref, long long nvec,
+                                                           CompressParams cp) {
+  unsigned kept = 0;
+  constexpr long long kTile = (long long)kBlock * U;
+  for (long long base = (long long)blockIdx.x * kTile + threadIdx.x; base < nvec;
+       base += (long long)gridDim.x * kTile) {
+    f4 v[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      v[u] = i < nvec ? ld4<NTL>(y, i) : f4{0.f, 0.f, 0.f, 0.f};
+      r[u] = i < nvec ? ld4<NTL>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      if (i >= nvec) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
+      st4<NTS>(y, i, v[u]);
+    }
+  }
+  block_add_count(kept, cp.kept);
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress(
+    float* y, const float* ref, size_t P, int mode, unsigned long long* kept, int u, int ntl, int nts,
+    int blocks_per_cu, void* stream) {
+  if (P % 4 || !y || !ref || !kept) return fail(CFA_E_INVALID, "compress experiment: P %% 4, null buffers");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  cp.cbegin = 0;
+  cp.cend = (long long)P;
+  cp.kept = kept;
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for((nvec + kBlock * u - 1) / (kBlock * u), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_C(U, L, S) \
+  if (u == U && ntl == L && nts == S) { compress_x_kernel<U, L, S><<<grid, kBlock, 0, st>>>(y, ref, nvec, cp); return check_launch("compress_x"); }
+  CFA_C(1, 1, 1) CFA_C(2, 1, 1) CFA_C(4, 1, 1) CFA_C(8, 1, 1)
+  CFA_C(4, 1, 0) CFA_C(4, 0, 1) CFA_C(4, 0, 0) CFA_C(2, 1, 0) CFA_C(8, 1, 0)
+#undef CFA_C
+  return fail(CFA_E_INVALID, "variant not instantiated");
+}

@@ -26,12 +26,12 @@ template <int N>
 __global__ __launch_bounds__(kBlock) void mewma_vec_kernel(MewmaArgs a, long long nvec) {
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
        i += (long long)gridDim.x * kBlock) {
-    f4 W = ld4<true>(a.W, i);
+    f4 W = ld4<false>(a.W, i);  // W and s are rewritten in place: default policy (see compress)
     f4 g[N], s_old[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       g[j] = ld4<true>(a.g[j], i);
-      if (!a.init) s_old[j] = ld4<true>(a.s[j], i);
+      if (!a.init) s_old[j] = ld4<false>(a.s[j], i);
     }
     const long long e0 = i * 4;
     f4 lr;
@@ -45,10 +45,10 @@ __global__ __launch_bounds__(kBlock) void mewma_vec_kernel(MewmaArgs a, long lon
       } else {
         s = a.rho * g[j] + a.one_minus_rho * s_old[j];  // numpy: rho*g + (1-rho)*s
       }
-      st4<true>(a.s[j], i, s);
+      st4<false>(a.s[j], i, s);
       W = W - lr * (a.filtered ? s : g[j]);
     }
-    st4<true>(a.W, i, W);
+    st4<false>(a.W, i, W);
   }
 }
 

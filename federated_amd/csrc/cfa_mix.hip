@@ -185,8 +185,10 @@ __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float*
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = base + (long long)u * kBlock;
-      v[u] = i < nvec ? ld4<true>(y, i) : f4{0.f, 0.f, 0.f, 0.f};
-      r[u] = (i < nvec && ref) ? ld4<true>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
+      // default-policy loads and stores: y is read and rewritten in place, and keeping its lines
+      // in L2 between the two lets the store merge (13% faster than nontemporal, compress_sweep)
+      v[u] = i < nvec ? ld4<false>(y, i) : f4{0.f, 0.f, 0.f, 0.f};
+      r[u] = (i < nvec && ref) ? ld4<false>(ref, i) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float*
       if (i >= nvec) continue;
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
-      st4<true>(y, i, v[u]);  // in place: an sc1 store measured 20% slower here
+      st4<false>(y, i, v[u]);  // in place: an sc1 store measured 20% slower, nt 13% slower
     }
   }
   for (long long i = 4 * nvec + (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += stride) {
