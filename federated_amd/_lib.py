@@ -113,6 +113,12 @@ SIGNATURES = {
                                    ctypes.POINTER(_c_size_t), _c_int_p, _c_int, _c_void_p]),
     "cfa_allreduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_reduce_sum_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
+    "cfa_mat_read": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_c_void_p)]),
+    "cfa_mat_free": (None, [_c_void_p]),
+    "cfa_mat_num_vars": (_c_int, [_c_void_p]),
+    "cfa_mat_vars": (_c_void_p, [_c_void_p]),
+    "cfa_mat_header": (ctypes.c_char_p, [_c_void_p]),
+    "cfa_mat_write": (_c_int, [ctypes.c_char_p, ctypes.c_char_p, _c_int, _c_void_p]),
     "cfa_payload_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
     "cfa_payload_free": (None, [_c_void_p]),
     "cfa_host_device_pointer": (_c_int, [_c_void_p, _PP]),

@@ -116,6 +116,36 @@ CFA_API const char* cfa_last_error(void);
  * calling thread's current device is restored. Idempotent. */
 CFA_API int cfa_device_prepare(int device);
 
+/* ---------------------------------------------------------------------------------------
+ * (f2) MATLAB level-5 files of the TF1 exchange (host only). Every TF1 consensus call publishes
+ * its model with scipy.io.savemat and loads its neighbours' with scipy.io.loadmat
+ * (TF1/consensus/cfa.py:108-117, 131-139; cfa_ongraphs.py:214-223, 282-291;
+ * cfa_ge_2stage.py:537-606). cfa_mat_write writes the bytes scipy's level-5 writer writes for real
+ * numeric matrices (uncompressed, column-major data, 8-byte padding, small-data elements at <= 4
+ * bytes); cfa_mat_read parses such files (scipy's or MATLAB's, uncompressed, little-endian,
+ * real numeric classes only) and returns CFA_E_UNSUPPORTED for anything else, so the caller can
+ * fall back to scipy. The parsed file owns the memory its variables point into.
+ */
+#define CFA_MAT_MAX_DIM 8
+typedef struct {
+  const char* name;
+  int mat_class;   /* mxDOUBLE_CLASS = 6, SINGLE 7, INT8 8, UINT8 9, INT16 10, UINT16 11, INT32 12,
+                      UINT32 13, INT64 14, UINT64 15 */
+  int mi_type;     /* stored element type: miINT8 1, miUINT8 2, miINT16 3, miUINT16 4, miINT32 5,
+                      miUINT32 6, miSINGLE 7, miDOUBLE 9, miINT64 12, miUINT64 13 */
+  int ndim;
+  int64_t dims[CFA_MAT_MAX_DIM];
+  const void* data; /* column-major elements of mi_type */
+  size_t nbytes;
+} cfa_mat_var_t;
+typedef struct cfa_mat cfa_mat_t;
+CFA_API int cfa_mat_read(const char* path, cfa_mat_t** out);
+CFA_API void cfa_mat_free(cfa_mat_t* mat);
+CFA_API int cfa_mat_num_vars(const cfa_mat_t* mat);
+CFA_API const cfa_mat_var_t* cfa_mat_vars(const cfa_mat_t* mat);
+CFA_API const char* cfa_mat_header(const cfa_mat_t* mat);
+CFA_API int cfa_mat_write(const char* path, const char* header, int nvars, const cfa_mat_var_t* vars);
+
 /* Host-path helpers (the per-call drop-in path): hipStreamSynchronize, and a
  * stream-ordered fetch of a device uint64 counter (e.g. a compression kept_count) into host
  * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero; and one

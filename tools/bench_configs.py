@@ -23,7 +23,7 @@ import numpy as np  # noqa: E402
 import scipy.io as sio  # noqa: E402
 import torch  # noqa: E402
 
-from federated_amd import topology as T  # noqa: E402
+from federated_amd import matfile, topology as T  # noqa: E402
 from federated_amd.engine import get_engine  # noqa: E402
 from oracle import cfa_oracle as O  # noqa: E402
 
@@ -74,12 +74,19 @@ def tf1_call(shapes, K, N, module, reps=20, **kw):
                 if module != "cfa" and kw["compression"]:
                     O.tf1_compress(np.asarray(out[2], dtype=np.float64), local[2], kw["compression"])
             t_np = med_time(numpy_path, reps)
-            t_io = med_time(lambda: [sio.loadmat(f"datamat{int(j)}_0.mat") for j in nbr], reps)
+            t_io = med_time(lambda: [matfile.loadmat(f"datamat{int(j)}_0.mat") for j in nbr], reps)
+            t_io_scipy = med_time(lambda: [sio.loadmat(f"datamat{int(j)}_0.mat") for j in nbr], reps)
+            save = {"weights1": local[0], "biases1": local[1], "weights2": local[2], "biases2": local[3],
+                    "epoch": 1, "loss_sample": np.zeros(3), "counter_param": 1}
+            t_save = med_time(lambda: matfile.savemat("bench_save.mat", save), reps)
+            t_save_scipy = med_time(lambda: sio.savemat("bench_save.mat", save), reps)
         finally:
             os.chdir(old)
     P = sum(int(np.prod(s)) for s in shapes)
     return {"P": P, "neighbours": len(nbr), "dropin_call_ms": round(t_call * 1e3, 3),
-            "of_which_mat_loads_ms": round(t_io * 1e3, 3), "numpy_arith_ms": round(t_np * 1e3, 3)}
+            "of_which_mat_loads_ms": round(t_io * 1e3, 3), "scipy_loadmat_ms": round(t_io_scipy * 1e3, 3),
+            "of_which_mat_save_ms": round(t_save * 1e3, 3), "scipy_savemat_ms": round(t_save_scipy * 1e3, 3),
+            "numpy_arith_ms": round(t_np * 1e3, 3)}
 
 
 def population(D, P, lists, policy, reps=20, use_window=None):
@@ -260,13 +267,19 @@ def main():
         for r in rows:
             print(json.dumps(r), flush=True)
         return
-    rows.append({"config": "CPU pool baseline: 8 x 25M mix, one process per device", **cpu_pool_round()})
+    dropin_only = len(sys.argv) > 1 and sys.argv[1] == "dropin"
+    if not dropin_only:
+        rows.append({"config": "CPU pool baseline: 8 x 25M mix, one process per device", **cpu_pool_round()})
     rows.append({"config": "C1 2NN, 4 devices, cfa.py (federated_sample_2NN_CFA.py)",
                  **tf1_call([(512, 32), (32,), (32, 8), (8,)], 4, 2, "cfa")})
     rows.append({"config": "C2 CNN FL_CFA_CNN_tf2 shapes, 8 devices, K=3, cfa_ongraphs mode 1, compression 2",
                  **tf1_call([(3, 3, 1, 4), (4,), (4096, 6), (6,)], 8, 3, "ongraphs", compression=2)})
     rows.append({"config": "C3 CFA-GE CNN, 16 devices, N=2 (stage-1 mix via cfa.py math)",
                  **tf1_call([(16, 1, 8), (8,), (168, 8), (8,)], 16, 2, "cfa")})
+    if dropin_only:
+        for r in rows:
+            print(json.dumps(r), flush=True)
+        return
     rows.append({"config": "C1 shapes as a device-resident TF1 population (Tf1PopulationRound), 4 devices, N=2",
                  **tf1_population(4, 16_680, 2, 1.0)})
     rows.append({"config": "C3 topology as a device-resident TF1 population (stage-1 mix only), 16 devices, N=2",
