@@ -119,6 +119,12 @@ SIGNATURES = {
     "cfa_mat_vars": (_c_void_p, [_c_void_p]),
     "cfa_mat_header": (ctypes.c_char_p, [_c_void_p]),
     "cfa_mat_write": (_c_int, [ctypes.c_char_p, ctypes.c_char_p, _c_int, _c_void_p]),
+    "cfa_npy_read": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_c_void_p)]),
+    "cfa_npy_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
+    "cfa_npy_free": (None, [_c_void_p]),
+    "cfa_npy_kind": (_c_int, [_c_void_p]),
+    "cfa_npy_num_arrays": (_c_int, [_c_void_p]),
+    "cfa_npy_arrays": (_c_void_p, [_c_void_p]),
     "cfa_payload_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
     "cfa_payload_free": (None, [_c_void_p]),
     "cfa_host_device_pointer": (_c_int, [_c_void_p, _PP]),

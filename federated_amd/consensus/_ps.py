@@ -13,6 +13,7 @@ import random
 
 import numpy as np
 
+from .. import npyfile
 from ._runtime import mixer, pause
 
 
@@ -29,14 +30,15 @@ def fedavg_into(params, models, update_factor, divide=True):
 
 
 def load_retry(path):
-    """np.load of a peer's published object array with one retry after pause(5)."""
+    """np.load of a peer's published object array (native reader, federated_amd/npyfile.py) with
+    one retry after pause(5)."""
     try:
-        return np.load(path, allow_pickle=True), True
+        return npyfile.load(path), True
     except Exception:
         pause(5)
         print("retrying opening model on server")
         try:
-            return np.load(path, allow_pickle=True), True
+            return npyfile.load(path), True
         except Exception:
             print("halting aggregation on server")
             return None, False
@@ -69,12 +71,12 @@ class PSBase:
                 print("waiting on server")
                 pause(1)
             try:
-                self.loss[k] = np.load(self.outfile[k], allow_pickle=True)["loss"]
+                self.loss[k] = npyfile.load(self.outfile[k])["loss"]
             except Exception:
                 pause(5)
                 print("retrying opening variables on server")
                 try:
-                    self.loss[k] = np.load(self.outfile[k], allow_pickle=True)["loss"]
+                    self.loss[k] = npyfile.load(self.outfile[k])["loss"]
                 except Exception:
                     print("failed opening variables on server")
         best = np.argmax(self.loss)
@@ -83,12 +85,12 @@ class PSBase:
             print("waiting")
             pause(1)
         try:
-            w = np.load(self.outfile_models[int(best)], allow_pickle=True)
+            w = npyfile.load(self.outfile_models[int(best)])
         except Exception:
             pause(5)
             print("retrying opening model")
             try:
-                w = np.load(self.outfile_models[int(best)], allow_pickle=True)
+                w = npyfile.load(self.outfile_models[int(best)])
             except Exception:
                 print("halting aggregation")
                 stop = True

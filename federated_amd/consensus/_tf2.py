@@ -18,6 +18,7 @@ import os
 
 import numpy as np
 
+from .. import npyfile
 from . import _tf1
 from ._runtime import mixer, pause
 
@@ -43,7 +44,7 @@ def tx_ring(ii, neighbors, devices):
 
 
 def _load_vars(outfile, count_key):
-    d = np.load(outfile, allow_pickle=True)
+    d = npyfile.load(outfile)
     return d[count_key], d["training_end"]
 
 
@@ -134,12 +135,12 @@ class TF2Base:
                 except Exception:
                     print("problems loading variables")
         try:
-            return np.load(outfile_models, allow_pickle=True), True
+            return npyfile.load(outfile_models), True
         except Exception:
             pause(5)
             print("retrying opening model")
             try:
-                return np.load(outfile_models, allow_pickle=True), True
+                return npyfile.load(outfile_models), True
             except Exception:
                 print("failed to load model federation")
                 return [], False

@@ -8,6 +8,7 @@ import random
 
 import numpy as np
 
+from .. import npyfile
 from ._ps import PSBase, fedavg_into, load_retry
 from ._runtime import pause
 
@@ -21,7 +22,7 @@ class Parameter_Server(PSBase):
         self.epoch_count = 0
 
     def _load_status(self, k):
-        d = np.load(self.outfile[k], allow_pickle=True)
+        d = npyfile.load(self.outfile[k])
         return d["epoch_count"], d["training_end"]
 
     def federated_target_weights_aggregation(self, epoch, aggregation_type=0):

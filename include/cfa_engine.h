@@ -146,6 +146,42 @@ CFA_API const cfa_mat_var_t* cfa_mat_vars(const cfa_mat_t* mat);
 CFA_API const char* cfa_mat_header(const cfa_mat_t* mat);
 CFA_API int cfa_mat_write(const char* path, const char* header, int nvars, const cfa_mat_var_t* vars);
 
+/* ---------------------------------------------------------------------------------------
+ * (f2) numpy files of the TF2 exchange (host only). The TF2 consensus / parameter-server modules
+ * load each neighbour's status archive and model with np.load(..., allow_pickle=True)
+ * (TF2/MNIST_dataset/consensus/consensus_v3.py:82-141, consensus_v4.py:30-95,
+ * parameter_server_v2.py:83-164): results/dump_train_variables{k}.npz (np.savez, stored zip of
+ * numeric .npy members) and results/dump_train_model{k}.npy (np.save of a 1-D object array of
+ * per-layer ndarrays, i.e. a pickle). cfa_npy_read reads one file and locates its arrays in place:
+ * a numeric .npy (kind CFA_NPY_ARRAY, one array), an object .npy whose pickle holds only numpy's
+ * ndarray reconstructors and numeric elements (CFA_NPY_OBJECT, one array per element; nothing in
+ * the file is executed), or a stored .npz of numeric members (CFA_NPY_ARCHIVE, CRC-checked, one
+ * array per member, named without ".npy"). Anything else returns CFA_E_UNSUPPORTED (fall back to
+ * np.load); truncated or corrupt files return CFA_E_INVALID. The parsed file owns the memory its
+ * arrays point into.
+ */
+#define CFA_NPY_MAX_DIM 32
+enum { CFA_NPY_ARRAY = 0, CFA_NPY_OBJECT = 1, CFA_NPY_ARCHIVE = 2 };
+typedef struct {
+  const char* name;   /* archive member name (without ".npy"); NULL for .npy files */
+  const char* descr;  /* numpy dtype string: "<f4", "<f8", "<i8", "|b1", "|u1", ... */
+  int itemsize;
+  int ndim;
+  int64_t shape[CFA_NPY_MAX_DIM];
+  int fortran_order;
+  const void* data;   /* elements in C order, or Fortran order when fortran_order */
+  size_t nbytes;
+} cfa_npy_array_t;
+typedef struct cfa_npy cfa_npy_t;
+CFA_API int cfa_npy_read(const char* path, cfa_npy_t** out);
+/* The same on a file image already in memory; the arrays point into `image`, which the caller
+ * keeps alive until cfa_npy_free. */
+CFA_API int cfa_npy_parse(const void* image, size_t nbytes, cfa_npy_t** out);
+CFA_API void cfa_npy_free(cfa_npy_t* npy);
+CFA_API int cfa_npy_kind(const cfa_npy_t* npy);
+CFA_API int cfa_npy_num_arrays(const cfa_npy_t* npy);
+CFA_API const cfa_npy_array_t* cfa_npy_arrays(const cfa_npy_t* npy);
+
 /* Host-path helpers (the per-call drop-in path): hipStreamSynchronize, and a
  * stream-ordered fetch of a device uint64 counter (e.g. a compression kept_count) into host
  * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero; and one
