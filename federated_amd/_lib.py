@@ -119,6 +119,9 @@ SIGNATURES = {
     "cfa_mat_vars": (_c_void_p, [_c_void_p]),
     "cfa_mat_header": (ctypes.c_char_p, [_c_void_p]),
     "cfa_mat_write": (_c_int, [ctypes.c_char_p, ctypes.c_char_p, _c_int, _c_void_p]),
+    "cfa_host_mix_staging_elems": (_c_size_t, [_c_void_p, _c_int, _c_int, _c_size_t]),
+    "cfa_host_mix_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p,
+                                  _c_void_p, _c_size_t, _c_void_p, _c_size_t, _c_int, _c_void_p]),
     "cfa_npy_read": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_c_void_p)]),
     "cfa_npy_parse": (_c_int, [_c_void_p, _c_size_t, ctypes.POINTER(_c_void_p)]),
     "cfa_npy_free": (None, [_c_void_p]),

@@ -29,16 +29,16 @@ def fedavg_into(params, models, update_factor, divide=True):
         params[q] = out[q].reshape(np.shape(local[q]))
 
 
-def load_retry(path):
+def load_retry(path, slot=None):
     """np.load of a peer's published object array (native reader, federated_amd/npyfile.py) with
-    one retry after pause(5)."""
+    one retry after pause(5); ``slot`` as in npyfile.load (models the aggregation consumes)."""
     try:
-        return npyfile.load(path), True
+        return npyfile.load(path, slot=slot), True
     except Exception:
         pause(5)
         print("retrying opening model on server")
         try:
-            return npyfile.load(path), True
+            return npyfile.load(path, slot=slot), True
         except Exception:
             print("halting aggregation on server")
             return None, False

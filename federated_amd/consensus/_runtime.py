@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import threading
 import time
@@ -103,7 +104,11 @@ def _layout_of(arrays) -> BucketLayout:
     return lay
 
 
-PIPELINE_MIN_BYTES = 64 << 20     # host mixes with more staging than this take the chunked pipeline
+NATIVE_PIPELINE = True            # fp32 host mixes above NATIVE_MIN_BYTES of staging: cfa_host_mix_f32
+NATIVE_MIN_BYTES = 1 << 20        # staging bytes from which the native chunk pipeline beats single-shot
+NATIVE_CHUNK_ELEMS = 128 << 10    # elements per model per native pipeline chunk
+NATIVE_THREADS = 0                # host copy threads of the native pipeline (0: torch.get_num_threads(), <= 4)
+PIPELINE_MIN_BYTES = 64 << 20     # (NATIVE_PIPELINE off) host mixes above this take the Python chunk pipeline
 PIPELINE_CHUNK_BYTES = 128 << 20  # staging bytes per pipeline chunk
 PIPELINE_ZERO_COPY = True          # pipeline chunks mixed in place in pinned host memory (no H2D/D2H)
 SINGLE_ZERO_COPY = True            # single-shot fp32 mixes read/write pinned staging in place (no H2D/D2H)
@@ -162,13 +167,19 @@ class HostMixer:
         moves by one async H2D copy and the result by one D2H (same kernels, same results).
         Returns (fp32 arrays with the local shapes, kept count or None).
 
-        Buckets above PIPELINE_MIN_BYTES of staging (without compression or the TF1 rule) take
-        the chunked pipeline ``_mix_pipelined`` instead: same kernels per chunk, same results."""
+        From NATIVE_MIN_BYTES of staging (without compression or the TF1 rule) the whole host path
+        runs as libcfa's chunk pipeline ``_mix_native`` instead (pack / PCIe kernel / unpack
+        overlapped chunk by chunk in one call; same kernels per chunk, same results); with
+        ``NATIVE_PIPELINE = False`` buckets above PIPELINE_MIN_BYTES take the Python pipeline
+        ``_mix_pipelined``."""
         layout = _layout_of(local)
         P, n = layout.P, len(nbrs)
         _check_coefficients(n, alphas, divisors)
-        if not tf1 and compress is None and n > 0 and (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
-            return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
+        if not tf1 and compress is None and n > 0:
+            if NATIVE_PIPELINE and (n + 1) * P * 4 >= NATIVE_MIN_BYTES:
+                return self._mix_native(layout, local, nbrs, alphas, divisors), None
+            if (n + 1) * P * 4 >= PIPELINE_MIN_BYTES:
+                return self._mix_pipelined(layout, local, nbrs, alphas, divisors), None
         st = self._stream()
         if SINGLE_ZERO_COPY:
             return self._mix_zero_copy(layout, local, nbrs, alphas, divisors, st, compress, tf1)
@@ -279,6 +290,40 @@ class HostMixer:
             dev = self.engine.device
             s = self._tls.aux = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
         return s
+
+    def _mix_native(self, layout: BucketLayout, local, nbrs, alphas, divisors,
+                    chunk_elems: Optional[int] = None, threads: Optional[int] = None) -> List[np.ndarray]:
+        """The whole host path in one libcfa call (``cfa_host_mix_f32``): chunk c of every model
+        is copied into pinned staging by a pool of host threads while the zero-copy kernel of
+        chunk c - 1 reads over PCIe, and each chunk's result is copied into the output layers
+        as soon as it lands. Same kernels per chunk as the single-shot mix, same results."""
+        P, n, L = layout.P, len(nbrs), len(layout.sizes)
+        chunk = int(chunk_elems or NATIVE_CHUNK_ELEMS)
+        nthreads = int(threads or NATIVE_THREADS or min(4, torch.get_num_threads()))
+        keep, ins = [], (ctypes.c_void_p * ((n + 1) * L))()
+        for m, model in enumerate((local, *nbrs)):
+            if len(model) != L:
+                raise ValueError(f"expected {L} tensors, got {len(model)}")
+            for k, a in enumerate(model):
+                a = np.asarray(a)
+                if a.dtype != np.float32 or not a.flags.c_contiguous:
+                    a = np.ascontiguousarray(a, dtype=np.float32)
+                if a.size != layout.sizes[k]:
+                    raise ValueError(f"tensor {k} has {a.size} elements, layout expects {layout.sizes[k]}")
+                keep.append(a)
+                ins[m * L + k] = a.ctypes.data
+        outs = [np.empty(shp, dtype=np.float32) for shp in layout.shapes]
+        optr = (ctypes.c_void_p * L)(*[o.ctypes.data for o in outs])
+        sizes = (ctypes.c_size_t * L)(*layout.sizes)
+        need = self.engine.lib.cfa_host_mix_staging_elems(sizes, L, n, chunk)
+        staging = self._cached("h_native", need, pinned=True)
+        h_out = self._cached("h_out", P, pinned=True)
+        a_arr = _lib.float_array(list(alphas))
+        d_arr = _lib.float_array(list(divisors)) if divisors is not None else None
+        _lib.call("cfa_host_mix_f32", optr, ins, sizes, L, n, a_arr, d_arr, staging.data_ptr(), need,
+                  h_out.data_ptr(), chunk, nthreads, self.engine.stream_handle(self._stream()))
+        del keep
+        return outs
 
     def _mix_pipelined(self, layout: BucketLayout, local, nbrs, alphas, divisors) -> List[np.ndarray]:
         """Large host-resident mix as a chunk pipeline over three streams. Staging is

@@ -119,10 +119,11 @@ class TF2Base:
                 return False, None
         return True, nbr_count
 
-    def _wait_and_load(self, outfile, outfile_models, nbr_count, epoch_count, max_lag):
+    def _wait_and_load(self, outfile, outfile_models, nbr_count, epoch_count, max_lag, slot=None):
         """Staleness wait (neighbour count < local count - max_lag and not training_end, status
         re-read each second with one retry), then the model load with one retry. Returns
-        (model, success)."""
+        (model, success). ``slot``: load into a reused buffer (npyfile.load), for models the
+        call consumes itself."""
         while not os.path.isfile(outfile_models) or nbr_count < epoch_count - max_lag and not self.training_end:
             pause(1)
             try:
@@ -135,12 +136,12 @@ class TF2Base:
                 except Exception:
                     print("problems loading variables")
         try:
-            return npyfile.load(outfile_models), True
+            return npyfile.load(outfile_models, slot=slot), True
         except Exception:
             pause(5)
             print("retrying opening model")
             try:
-                return npyfile.load(outfile_models), True
+                return npyfile.load(outfile_models, slot=slot), True
             except Exception:
                 print("failed to load model federation")
                 return [], False
@@ -158,7 +159,8 @@ class TF2Base:
             if not ok:
                 break
             pause(round(np.random.random(), 2))
-            model, success = self._wait_and_load(outfile, outfile_models, nbr_count, epoch_count, max_lag)
+            model, success = self._wait_and_load(outfile, outfile_models, nbr_count, epoch_count, max_lag,
+                                                 slot=("tf2", q))
             if success:
                 loaded.append(model)
             if self.training_end and len(loaded) > 0:
@@ -172,8 +174,8 @@ class TF2Base:
             eps_t_control = 1 / (len(loaded) + 1)
             if self.training_end:
                 print("detected training end")
-                for k in range(self.layers):
-                    self.local_weights[k] = loaded[-1][k]
+                for k in range(self.layers):  # a copy: the loaded layers live in reused read buffers
+                    self.local_weights[k] = np.array(loaded[-1][k])
             else:
                 _mix_into(self.local_weights, loaded, eps_t_control)
         return self.local_weights.tolist()

@@ -27,7 +27,7 @@ class Parameter_Server(PSBase):
             while not os.path.isfile(paths[k]):
                 print("waiting")
                 pause(1)
-            m, ok = load_retry(paths[k])
+            m, ok = load_retry(paths[k], slot=("ps", len(models)))
             if ok:
                 models.append(m)
             else:

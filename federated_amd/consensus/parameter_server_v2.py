@@ -60,7 +60,7 @@ class Parameter_Server(PSBase):
                         nbr_count, self.training_end[k] = self._load_status(k)
                     except Exception:
                         print("failed opening variables on server")
-            m, ok = load_retry(self.outfile_models[k])
+            m, ok = load_retry(self.outfile_models[k], slot=("ps", len(models)))
             if ok:
                 models.append(m)
             else:

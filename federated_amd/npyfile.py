@@ -16,11 +16,17 @@ read-only mapping of member name -> array (``NpzFile``'s ``[]``, ``files``, ``ke
 ``close()`` and ``with``). Files outside the reader's scope (compressed archives, structured or
 big-endian dtypes, other pickled objects) go to ``np.load`` unchanged; a truncated or corrupt
 file raises, as ``np.load`` does.
+
+``load(path, slot=key)`` reads into a per-thread buffer kept under ``key`` instead of a fresh one
+(no page faults on every read): the arrays it returns are valid only until the next load with
+the same key on the same thread. The drop-in's neighbour loops use it for the models they
+consume within the call (the mix copies them out); anything handed back to the caller is copied.
 """
 from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from collections.abc import Mapping
 
 import numpy as np
@@ -64,19 +70,35 @@ class Archive(Mapping):
         self.close()
 
 
-def _read_image(path) -> np.ndarray:
+_tls = threading.local()
+
+
+def _slot_buffer(slot, size: int) -> np.ndarray:
+    bufs = getattr(_tls, "bufs", None)
+    if bufs is None:
+        bufs = _tls.bufs = {}
+    b = bufs.get(slot)
+    if b is None or b.size < size:
+        if len(bufs) >= 64:  # bounded: one buffer per neighbour slot in practice
+            bufs.clear()
+        b = bufs[slot] = np.empty(size + (size >> 3), dtype=np.uint8)  # headroom for growing files
+    return b[:size]
+
+
+def _read_image(path, slot=None) -> np.ndarray:
     """The file's bytes in one unbuffered read into an uninitialised numpy buffer (numpy's
-    allocator: no zero-fill pass over fresh pages, unlike bytearray(n))."""
+    allocator: no zero-fill pass over fresh pages, unlike bytearray(n)), or into the slot's
+    reused buffer."""
     with open(path, "rb", buffering=0) as f:
         size = os.fstat(f.fileno()).st_size
-        image = np.empty(size, dtype=np.uint8)
+        image = np.empty(size, dtype=np.uint8) if slot is None else _slot_buffer(slot, size)
         got = f.readinto(image) if size else 0
     return image[:got] if got != size else image
 
 
-def load(path):
+def load(path, slot=None):
     """np.load(path, allow_pickle=True) for the TF2 exchange files (see the module docstring)."""
-    image = _read_image(path)
+    image = _read_image(path, slot)
     lib = _lib.load()
     handle = ctypes.c_void_p()
     start = image.ctypes.data

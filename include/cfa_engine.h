@@ -182,6 +182,24 @@ CFA_API int cfa_npy_kind(const cfa_npy_t* npy);
 CFA_API int cfa_npy_num_arrays(const cfa_npy_t* npy);
 CFA_API const cfa_npy_array_t* cfa_npy_arrays(const cfa_npy_t* npy);
 
+/* (f2) The drop-in host path of one mix as a native chunk pipeline: the local model and n
+ * neighbour models arrive as per-layer fp32 arrays in pageable host memory (TF2
+ * consensus_v3.py:144-157 over the loaded .npy layer lists; parameter_server_v2.py:159-161) and
+ * the result goes back into per-layer arrays. The bucket range is cut into chunks of
+ * chunk_elems; chunk c of every model is copied into `staging` (pinned host, chunk-major, slices
+ * padded to 4 elements) by `threads` host threads while the kernel of chunk c - 1 reads its
+ * slices over PCIe in place; each chunk's result lands in `out_pinned` (pinned host, P elements)
+ * and is copied into out_layers as soon as its kernel is done. Each chunk runs cfa_mix_seq_f32
+ * when divisors is NULL, else cfa_mix_seq_div_f32, so the result equals the single-shot mix
+ * bit for bit. in_layers is model-major: model m (0 = local), layer k at
+ * [m * L + k]. Returns when every output layer is written.
+ * cfa_host_mix_staging_elems gives the staging size one call needs. */
+CFA_API size_t cfa_host_mix_staging_elems(const size_t* layer_elems, int L, int n, size_t chunk_elems);
+CFA_API int cfa_host_mix_f32(float* const* out_layers, const float* const* in_layers,
+                             const size_t* layer_elems, int L, int n, const float* alphas,
+                             const float* divisors, float* staging, size_t staging_elems,
+                             float* out_pinned, size_t chunk_elems, int threads, void* stream);
+
 /* Host-path helpers (the per-call drop-in path): hipStreamSynchronize, and a
  * stream-ordered fetch of a device uint64 counter (e.g. a compression kept_count) into host
  * memory (pinned, for an asynchronous copy) followed by resetting the counter to zero; and one

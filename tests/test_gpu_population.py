@@ -285,6 +285,7 @@ def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide, zero_co
     result bit for bit, across layer boundaries and ragged tails."""
     from federated_amd.consensus import _runtime as R
     monkeypatch.setattr(R, "PIPELINE_ZERO_COPY", zero_copy)
+    monkeypatch.setattr(R, "NATIVE_PIPELINE", False)
     rng = np.random.default_rng(21)
     shapes = [(1001, 333), (333,), (517, 129), (7,)]
     local = [rng.standard_normal(s).astype(np.float32) for s in shapes]
@@ -302,6 +303,70 @@ def test_hostmixer_pipeline_equals_single_shot(gpu, monkeypatch, divide, zero_co
     flat = lambda m: np.concatenate([x.reshape(-1) for x in m])
     if not divide:
         assert np.array_equal(flat(got), sequential_mix(flat(local), [flat(m) for m in nbrs], al))
+
+
+@pytest.mark.parametrize("divide", [False, True])
+@pytest.mark.parametrize("chunk,threads", [(4, 1), (1000, 3), (65_536, 8), (1 << 22, 16)])
+def test_hostmixer_native_pipeline_equals_single_shot(gpu, monkeypatch, divide, chunk, threads):
+    """cfa_host_mix_f32 (pack by host threads / zero-copy kernel / unpack, chunk by chunk, one
+    call) returns the single-shot result bit for bit: chunks from 4 elements (every layer boundary
+    inside a chunk, thousands of chunks) to one chunk, 1 to 16 copy threads, the FedAvg divisor
+    form, fp64 and non-contiguous inputs, an empty layer."""
+    from federated_amd.consensus import _runtime as R
+    rng = np.random.default_rng(22)
+    shapes = [(1001, 333), (0,), (333,), (517, 129), (7,)] if chunk > 4 else [(61, 33), (0,), (5,), (7,)]
+    local = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    nbrs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(3)]
+    nbrs[1][0] = nbrs[1][0].astype(np.float64)                       # converted like the single shot
+    nbrs[2][0] = np.asfortranarray(nbrs[2][0])                       # non-C-contiguous
+    al = [0.25, 0.5, 0.125]
+    div = [4.0, 4.0, 4.0] if divide else None
+    mx = R.mixer()
+    monkeypatch.setattr(R, "NATIVE_PIPELINE", False)
+    ref, _ = mx.mix(local, nbrs, al, divisors=div)
+    monkeypatch.setattr(R, "NATIVE_PIPELINE", True)
+    monkeypatch.setattr(R, "NATIVE_MIN_BYTES", 0)
+    got = mx._mix_native(R._layout_of(local), local, nbrs, al, div, chunk_elems=chunk, threads=threads)
+    for a, r, s in zip(got, ref, shapes):
+        assert a.shape == s and a.dtype == np.float32 and np.array_equal(a, r)
+    got2, kept = mx.mix(local, nbrs, al, divisors=div)  # the dispatch takes the native path
+    assert kept is None and all(np.array_equal(a, r) for a, r in zip(got2, ref))
+
+
+def test_hostmixer_native_pipeline_concurrent_threads(gpu):
+    """Driver threads (FL_threads_CIFAR100.py runs one per device) calling the native pipeline at
+    once: the copy pool serves one call at a time and the others copy on their own thread; every
+    result equals its single-threaded one."""
+    import threading
+    from federated_amd.consensus import _runtime as R
+    shapes = [(700, 300), (300,), (300, 40), (40,)]
+    jobs = []
+    for t in range(6):
+        rng = np.random.default_rng(100 + t)
+        local = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+        nbrs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(2 + t % 3)]
+        jobs.append((local, nbrs, [1.0 / (len(nbrs) + 1)] * len(nbrs)))
+    mx = R.mixer()
+    want = [mx._mix_native(R._layout_of(l), l, nb, al, None, chunk_elems=50_000, threads=1) for l, nb, al in jobs]
+    got = [None] * len(jobs)
+    errors = []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(gpu.device)
+            l, nb, al = jobs[i]
+            for _ in range(5):
+                got[i] = mx._mix_native(R._layout_of(l), l, nb, al, None, chunk_elems=50_000, threads=8)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=60)
+    assert not errors, errors
+    for g, w in zip(got, want):
+        assert all(np.array_equal(a, b) for a, b in zip(g, w))
 
 
 def test_bench_shape_round_full_buckets(gpu):

@@ -276,3 +276,21 @@ def test_reader_under_address_sanitizer():
     r = subprocess.run(["bash", script, "3000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "no finding" in r.stdout
+
+
+def test_slot_loads_reuse_one_buffer(tmp_path):
+    """load(path, slot=k) reads into the slot's reused buffer: same values as a fresh load; the
+    arrays of the previous load with that slot are overwritten by the next one (the contract the
+    drop-in's neighbour loops rely on), other slots are untouched."""
+    a, b = tmp_path / "a.npy", tmp_path / "b.npy"
+    wa, wb = keras_weights([(40, 3), (3,)]), keras_weights([(40, 3), (3,)])
+    np.save(a, wa, allow_pickle=True)
+    np.save(b, wb, allow_pickle=True)
+    x = npyfile.load(str(a), slot=("t", 0))
+    same(wa, x)
+    y = npyfile.load(str(b), slot=("t", 1))
+    same(wa, x)  # another slot: x intact
+    z = npyfile.load(str(b), slot=("t", 0))
+    same(wb, z)
+    assert np.shares_memory(x[0], z[0]) and np.array_equal(x[0], wb[0])  # x now shows b's bytes
+    same(wb, y)

@@ -3,7 +3,7 @@
 model (CIFAR-100 VGG-1, P = 1 071 748, K = 4 neighbours) and of the FedAvg parameter server
 (parameter_server_v2, 8 active devices), with the protocol sleeps off (FEDERATED_AMD_PAUSE_SCALE=0):
 the whole call, and its file loads alone, with libcfa's .npy/.npz reader (the default) and with
-np.load in its place. Also the radar CNN (C5's TF2 shapes, P = 3 745 446).
+fresh read buffers, and with np.load in its place. Also the radar CNN (C5's TF2 shapes, P = 3 745 446).
 
 Usage: python tools/probe/tf2_calls.py [--reps 30]"""
 import argparse
@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import numpy as np  # noqa: E402
 
 from federated_amd import npyfile  # noqa: E402
-from federated_amd.consensus import _ps, _tf2, consensus_v3, parameter_server_v2  # noqa: E402
+from federated_amd.consensus import _ps, _runtime as R, _tf2, consensus_v3, parameter_server_v2  # noqa: E402
 
 VGG1 = [(3, 3, 3, 32), (32,), (3, 3, 32, 32), (32,), (8192, 128), (128,), (128, 100), (100,)]
 RADAR = [(8, 8, 1, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, 64), (64,), (7168, 512), (512,), (512, 6), (6,)]
@@ -42,11 +42,33 @@ def weights(shapes, rng):
     return w
 
 
-def use_np_load(on):
-    """Swap the drop-in's loader between libcfa's reader and np.load."""
-    fn = (lambda p: np.load(p, allow_pickle=True)) if on else npyfile.load
+MODES = {
+    "native": None,                                                   # libcfa's reader, slot buffers
+    "native_t4": None,                                                # the same, 4 pipeline copy threads
+    "native_t1": None,                                                # the same, 1 pipeline copy thread
+    "native_fresh": lambda p, slot=None: npyfile.load(p),             # libcfa's reader, fresh buffers
+    "np_load": lambda p, slot=None: np.load(p, allow_pickle=True),    # the reference's loader
+}
+
+
+def interleaved(fns, reps, rounds=6):
+    """Median over `rounds` interleaved passes of every mode (A B C A B C ...), each pass the
+    median of reps // rounds calls: slow drifts of the host hit every mode alike."""
+    acc = {m: {k: [] for k in fns} for m in MODES}
+    for _ in range(rounds):
+        for m in MODES:
+            use_loader(m)
+            for k, fn in fns.items():
+                acc[m][k].append(med(fn, max(3, reps // rounds)))
+    return {m: {k: round(statistics.median(v), 3) for k, v in d.items()} for m, d in acc.items()}
+
+
+def use_loader(mode):
+    """Swap the drop-in's loader (the modules call npyfile.load(path[, slot=...]))."""
+    fn = MODES[mode]
+    R.NATIVE_THREADS = {"native_t4": 4, "native_t1": 1}.get(mode, 0)
     for mod in (_tf2, _ps, parameter_server_v2):
-        mod.npyfile = type("L", (), {"load": staticmethod(fn)}) if on else npyfile
+        mod.npyfile = npyfile if fn is None else type("L", (), {"load": staticmethod(fn)})
 
 
 def tf2_call(shapes, K, reps):
@@ -68,12 +90,12 @@ def tf2_call(shapes, K, reps):
         for k in nbrs:
             d = _tf2.npyfile.load(f"results/dump_train_variables{k}.npz")
             d["epoch_count"], d["training_end"]
-            _tf2.npyfile.load(f"results/dump_train_model{k}.npy")
-    out = {}
-    for name, on in (("native", False), ("np_load", True)):
-        use_np_load(on)
-        out[name] = {"call_ms": round(med(call, reps), 3), "loads_ms": round(med(loads, reps), 3)}
-    use_np_load(False)
+            _tf2.npyfile.load(f"results/dump_train_model{k}.npy", slot=("tf2", k))
+    out = interleaved({"call_ms": call, "loads_ms": loads}, reps)
+    use_loader("native")
+    p.update_local_model(local.copy())
+    p.federated_weights_computing(nbrs, K, 5, 0.5)
+    assert p.local_weights[0] is not local[0]  # the mix ran (a failed load would skip it)
     return out
 
 
@@ -88,17 +110,14 @@ def ps_call(shapes, devices, reps):
 
     def call():
         ps.federated_target_weights_aggregation(1, aggregation_type=0)
-    out = {}
-    for name, on in (("native", False), ("np_load", True)):
-        use_np_load(on)
-        out[name] = {"call_ms": round(med(call, reps), 3)}
-    use_np_load(False)
+    out = interleaved({"call_ms": call}, reps)
+    use_loader("native")
     return out
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--reps", type=int, default=60)
     a = ap.parse_args()
     old = os.getcwd()
     with tempfile.TemporaryDirectory() as d:
