@@ -4,8 +4,10 @@
 # files). Usage: tools/asan/run_matfile_fuzz.sh [iters per seed]
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-OUT=${TMPDIR:-/tmp}/cfa_matfile_fuzz
-mkdir -p "$OUT"
+# Scratch on tmpfs, one directory per run: the harness rewrites its file thousands of times, which
+# blocks on a slow disk, and concurrent runs must not share it.
+OUT=$(mktemp -d /dev/shm/cfa_matfile_fuzz.XXXXXX)
+trap 'rm -rf "$OUT"' EXIT
 g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
     -I"$ROOT/include" "$ROOT/federated_amd/csrc/cfa_matfile.cpp" "$ROOT/tools/asan/matfile_fuzz.cpp" \
     -o "$OUT/matfile_fuzz"

@@ -4,8 +4,10 @@
 # Usage: tools/asan/run_npy_fuzz.sh [iters per seed]
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-OUT=${TMPDIR:-/tmp}/cfa_npy_fuzz
-mkdir -p "$OUT"
+# Scratch on tmpfs, one directory per run: the harness rewrites its file thousands of times, which
+# blocks on a slow disk, and concurrent runs must not share it.
+OUT=$(mktemp -d /dev/shm/cfa_npy_fuzz.XXXXXX)
+trap 'rm -rf "$OUT"' EXIT
 g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
     -I"$ROOT/include" "$ROOT/federated_amd/csrc/cfa_npy.cpp" "$ROOT/tools/asan/npy_fuzz.cpp" \
     -o "$OUT/npy_fuzz"

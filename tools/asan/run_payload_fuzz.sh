@@ -3,8 +3,10 @@
 # mutations of reference-shaped payloads written by CPython's pickle. Usage: tools/asan/run_payload_fuzz.sh [iters]
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
-OUT=${TMPDIR:-/tmp}/cfa_payload_fuzz
-mkdir -p "$OUT"
+# Scratch on tmpfs, one directory per run: the harness rewrites its file thousands of times, which
+# blocks on a slow disk, and concurrent runs must not share it.
+OUT=$(mktemp -d /dev/shm/cfa_payload_fuzz.XXXXXX)
+trap 'rm -rf "$OUT"' EXIT
 g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -pthread \
     -I"$ROOT/include" "$ROOT/federated_amd/csrc/cfa_payload.cpp" "$ROOT/tools/asan/payload_fuzz.cpp" \
     -o "$OUT/payload_fuzz"
