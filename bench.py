@@ -90,7 +90,36 @@ def parse():
                         "(the committed profiles/ value is reported instead)")
     p.add_argument("--e2e", action="store_true",
                    help="also measure the host-resident path (pinned H2D + mix + D2H) on rank 0")
+    p.add_argument("--watchdog-seconds", type=float, default=900.0,
+                   help="end the run with status 124 and the phase it was in if it has not finished "
+                        "after this long (a collective that never completes; 0 = off)")
     return p.parse_args()
+
+
+class Watchdog:
+    """Ends the process (status 124) with the phase it was stuck in if the run has not finished in
+    time. A collective that never completes on one rank (a peer that died inside RCCL, a
+    mismatched exchange) otherwise hangs every rank until an outer limit kills the job without
+    saying where; torch.distributed.run tears the other ranks down once this one exits."""
+
+    def __init__(self, seconds: float, rank: int):
+        import threading
+        self.phase, self.rank, self._done = "start-up", rank, threading.Event()
+        self.t0 = time.perf_counter()
+        if seconds > 0:
+            threading.Thread(target=self._watch, args=(seconds,), daemon=True).start()
+
+    def _watch(self, seconds):
+        if not self._done.wait(seconds):
+            print(f"[bench rank {self.rank}] FATAL: watchdog: not finished after {seconds:.0f} s, "
+                  f"stuck in phase '{self.phase}'", file=sys.stderr, flush=True)
+            os._exit(124)
+
+    def enter(self, phase: str) -> None:
+        self.phase = phase
+
+    def done(self) -> None:
+        self._done.set()
 
 
 def cpu_model() -> str:
@@ -362,6 +391,7 @@ def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
 
 def main():
     args = parse()
+    watchdog = Watchdog(args.watchdog_seconds, int(os.environ.get("RANK", "0")))
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
     import torch
@@ -379,7 +409,11 @@ def main():
     device = local_rank % ndev  # one rank per GPU; more ranks than GPUs only for rehearsal (torch transport)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        # bounded control-plane waits: a peer that never arrives fails the barrier instead of
+        # holding every rank for torch's 30-minute default
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=max(60.0, args.watchdog_seconds)))
 
     from federated_amd.engine import get_engine
     from federated_amd.population import make_ring_shard
@@ -393,6 +427,7 @@ def main():
 
     transport, comparable = None, True
     if world > 1:
+        watchdog.enter("open transport")
         try:
             transport, comparable = open_transport(args.transport, rank, world, device, args.allow_fallback)
         except TransportError as exc:
@@ -415,6 +450,7 @@ def main():
         seed_shard(shard, info, P)
         return shard, info
 
+    watchdog.enter(f"build {args.partition} shard")
     shard, info = build(args.partition)
     autotune = None
     if world > 1 and info.get("route", {}).get("relay") and not args.no_autotune:
@@ -422,6 +458,7 @@ def main():
         # a few rounds each after warm-up, max over ranks; the faster one is the one timed (the
         # cost model assumes every link runs at the same rate; this checks it on the node)
         tune_steps = 3
+        watchdog.enter("route autotune")
         t_rel, _, _ = run_leg(args, shard, world, tune_steps, args.warmup, timed_kernel=False)
         dshard, dinfo = build(args.partition, relay=False)
         t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
@@ -434,6 +471,7 @@ def main():
             del dshard
             autotune["chosen"] = "relayed"
         torch.cuda.empty_cache()
+    watchdog.enter("timed rounds")
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
@@ -455,6 +493,7 @@ def main():
                                        "element slices; routed halo between ranks holding the same slice"))
         for part, groups, note in extra:
             saved, args.device_groups = args.device_groups, groups
+            watchdog.enter(f"{part} leg")
             xshard, xinfo = build(part)
             args.device_groups = saved
             xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
@@ -469,6 +508,7 @@ def main():
             # weak form for reference: the single-GPU population on every rank (D = 128 N), the
             # same routed halo now hidden under 120 interior mixes per rank
             Dw = args.devices * world
+            watchdog.enter("weak leg")
             wshard, winfo = build("devices", Dw)
             wel, _, _ = run_leg(args, wshard, world, args.steps, args.warmup, timed_kernel=False)
             legs["weak"] = {"value": round(Dw * (K + 2) * P * 4 * args.steps / wel / 1e9, 2),
@@ -546,6 +586,7 @@ def main():
     if world > 1:
         dist.barrier()
     # CPU baselines: rank 0, N = 1 only (bounded samples).
+    watchdog.enter("baselines and report")
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(P, K, args.cpu_seconds)
@@ -569,6 +610,7 @@ def main():
         transport.close()
     if world > 1:
         dist.destroy_process_group()
+    watchdog.done()
 
 
 def rccl_version():

@@ -57,3 +57,17 @@ def test_live_traffic_without_profiler(monkeypatch, tmp_path):
     monkeypatch.setenv("PATH", str(tmp_path))
     val, note = bench.live_traffic(25_000_000, 8, timeout=60)
     assert val is None and "not on PATH" in note
+
+
+def test_watchdog_ends_a_stuck_run_with_its_phase():
+    """A run that never finishes (e.g. one rank stuck in a collective) exits with status 124 and
+    names the phase it was in; a run that finishes in time is left alone."""
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "w = bench.Watchdog(%s, 3); w.enter('timed rounds'); time.sleep(%s); w.done(); print('finished')")
+    stuck = subprocess.run([sys.executable, "-c", code % (ROOT, 0.5, 30)], capture_output=True, text=True,
+                           timeout=60)
+    assert stuck.returncode == 124
+    assert "[bench rank 3] FATAL: watchdog" in stuck.stderr and "'timed rounds'" in stuck.stderr
+    ok = subprocess.run([sys.executable, "-c", code % (ROOT, 30, 0.1)], capture_output=True, text=True, timeout=60)
+    assert ok.returncode == 0 and "finished" in ok.stdout
