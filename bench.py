@@ -90,6 +90,10 @@ def parse():
                         "(the committed profiles/ value is reported instead)")
     p.add_argument("--e2e", action="store_true",
                    help="also measure the host-resident path (pinned H2D + mix + D2H) on rank 0")
+    p.add_argument("--placement-candidates", type=int, default=4,
+                   help="allocate each population stack this many times and keep the fastest, timed "
+                        "with the population's own mix before the timed region (federated_amd/placement.py; "
+                        "1 = plain allocation)")
     p.add_argument("--watchdog-seconds", type=float, default=900.0,
                    help="end the run with status 124 and the phase it was in if it has not finished "
                         "after this long (a collective that never completes; 0 = off)")
@@ -440,7 +444,8 @@ def main():
                                       transport,
                                       eng, partition=partition, dev_groups=args.device_groups,
                                       relay=(not args.no_relay) if relay is None else relay,
-                                      staged=not args.no_stages, window_batch=args.window_batch)
+                                      staged=not args.no_stages, window_batch=args.window_batch,
+                                      placement_candidates=args.placement_candidates)
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -558,6 +563,7 @@ def main():
                                | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
                                   "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
                                   "autotune": autotune}) if route else None,
+                "placement": info.get("placement"),
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",

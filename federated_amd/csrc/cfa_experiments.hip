@@ -279,6 +279,70 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_free(void
   return CFA_OK;
 }
 
+// Experiment (not part of the public header): a device buffer through the virtual-memory API, for
+// tools/probe/vmm_placement.py: one reserved VA range backed by physical handles of `chunk` bytes
+// each (rounded up to the allocation granularity; 0 = one handle for the whole range), mapped in
+// order and made read-write for `device`. Freed with cfa_experimental_vmm_free(ptr, bytes, chunk).
+namespace {
+hipMemAllocationProp vmm_prop(int device) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  return prop;
+}
+size_t vmm_round(size_t x, size_t g) { return (x + g - 1) / g * g; }
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_vmm_granularity(int device, size_t* min_g,
+                                                                                       size_t* rec_g) {
+  hipMemAllocationProp prop = vmm_prop(device);
+  CFA_HIP_CHECK(hipMemGetAllocationGranularity(min_g, &prop, hipMemAllocationGranularityMinimum));
+  CFA_HIP_CHECK(hipMemGetAllocationGranularity(rec_g, &prop, hipMemAllocationGranularityRecommended));
+  return CFA_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_vmm_alloc(void** p, size_t bytes, size_t chunk,
+                                                                                 int device) {
+  if (!p || !bytes) return fail(CFA_E_INVALID, "vmm: bad arguments");
+  hipMemAllocationProp prop = vmm_prop(device);
+  size_t g = 0;
+  CFA_HIP_CHECK(hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended));
+  const size_t total = vmm_round(bytes, g);
+  const size_t step = chunk ? std::min(total, vmm_round(chunk, g)) : total;
+  void* base = nullptr;
+  CFA_HIP_CHECK(hipMemAddressReserve(&base, total, std::max<size_t>(g, size_t(1) << 30), nullptr, 0));
+  for (size_t off = 0; off < total; off += step) {
+    const size_t n = std::min(step, total - off);
+    hipMemGenericAllocationHandle_t h;
+    hipError_t e = hipMemCreate(&h, n, &prop, 0);
+    if (e == hipSuccess) {
+      e = hipMemMap(static_cast<char*>(base) + off, n, 0, h, 0);
+      (void)hipMemRelease(h);  // the mapping keeps the physical memory alive
+    }
+    if (e != hipSuccess) return fail(CFA_E_HIP, "vmm: create/map at %zu of %zu: %s", off, total, hipGetErrorString(e));
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  CFA_HIP_CHECK(hipMemSetAccess(base, total, &acc, 1));
+  *p = base;
+  return CFA_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_vmm_free(void* p, size_t bytes, size_t chunk,
+                                                                                int device) {
+  hipMemAllocationProp prop = vmm_prop(device);
+  size_t g = 0;
+  CFA_HIP_CHECK(hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended));
+  const size_t total = vmm_round(bytes, g);
+  const size_t step = chunk ? std::min(total, vmm_round(chunk, g)) : total;
+  for (size_t off = 0; off < total; off += step)
+    CFA_HIP_CHECK(hipMemUnmap(static_cast<char*>(p) + off, std::min(step, total - off)));
+  CFA_HIP_CHECK(hipMemAddressFree(p, total));
+  return CFA_OK;
+}
+
 
 // Experiment (not part of the public header): a whole run of ring-window devices mixed in ONE
 // streaming launch. Workgroups walk the (device, tile) space in order, so there is one launch

@@ -140,7 +140,8 @@ class RingPopulationShard:
     """Device-resident buckets of one shard plus its halo buffers, and the round itself."""
 
     def __init__(self, plan: RingShardPlan, P: int, device, transport=None, engine=None,
-                 dtype=torch.float32, window_batch: int = 0, route=None, rank: Optional[int] = None):
+                 dtype=torch.float32, window_batch: int = 0, route=None, rank: Optional[int] = None,
+                 stacks: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
         """``window_batch`` = B > 0 mixes B consecutive devices per ``cfa_mix_window_f32`` pass,
         loading each row of their shared window once (identical results); 0 = one streaming
         mix per device.
@@ -148,14 +149,25 @@ class RingPopulationShard:
         ``route`` (a ``halo.RoutePlan`` over the global ranks, e.g. from ``make_ring_shard``)
         replaces the single grouped exchange: the halo travels in stages over direct and relayed
         paths, and each boundary device mixes as soon as the stages it reads have landed.
-        ``rank`` is this shard's global rank in that plan (default ``plan.rank``)."""
+        ``rank`` is this shard's global rank in that plan (default ``plan.rank``).
+
+        ``stacks`` = (models, mixed): caller-allocated ``[L, P]`` stacks (e.g. placement-calibrated,
+        ``federated_amd.placement``) instead of fresh ones."""
         if window_batch and not (1 <= window_batch <= 8 and plan.hl <= 4 and plan.hr <= 4):
             raise ValueError("window_batch must be 1..8 with at most 4 neighbours per side")
         self.window_batch = int(window_batch)
         self.plan, self.P = plan, int(P)
         self.device = torch.device(device)
-        self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
-        self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
+        if stacks is not None:
+            for t in stacks:
+                same_dev = t.device.type == self.device.type and (self.device.index is None
+                                                                   or t.device.index == self.device.index)
+                if tuple(t.shape) != (plan.L, self.P) or t.dtype != dtype or not same_dev:
+                    raise ValueError(f"stacks must be [{plan.L}, {self.P}] {dtype} on {self.device}")
+            self.models, self.mixed = stacks
+        else:
+            self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
+            self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
         self.halo = {
             "left": torch.empty((plan.hl, self.P), dtype=dtype, device=self.device),
             "right": torch.empty((plan.hr, self.P), dtype=dtype, device=self.device),
@@ -311,14 +323,17 @@ class RingPopulationShard:
 def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: int, device,
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
-                    window_batch: int = 0, dtype=torch.float32):
+                    window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
     Returns (shard, info): ``shard.P`` is this rank's slice length and ``info`` holds the
     partition, its (Gd, Gp) shape, this rank's element slice [lo, hi) of every bucket and the
     route summary. ``relay`` spreads the halo over relayed xGMI paths; ``staged`` sends it row by
-    row so boundary devices mix as their rows land (both only matter when Gd > 1)."""
+    row so boundary devices mix as their rows land (both only matter when Gd > 1).
+    ``placement_candidates`` > 1 allocates the shard's stacks placement-calibrated
+    (``placement.calibrated_stacks``: the fastest of that many allocations each, timed with the
+    shard's own mix; ``info["placement"]`` holds the probe)."""
     from .halo import RoutePlan, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
@@ -331,10 +346,18 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
         route = RoutePlan(world, tr, relay=relay)
-    shard = RingPopulationShard(plan, bounds[p + 1] - bounds[p], device, transport, engine, dtype,
-                                window_batch, route=route, rank=rank)
+    Pr = bounds[p + 1] - bounds[p]
+    stacks, placement = None, None
+    if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":
+        from .placement import calibrated_stacks
+        models, mixed, placement = calibrated_stacks(L, Pr, device, engine, hl, hr, placement_candidates,
+                                                     dtype=dtype)
+        stacks = (models, mixed)
+    shard = RingPopulationShard(plan, Pr, device, transport, engine, dtype, window_batch, route=route, rank=rank,
+                                stacks=stacks)
     info = {"partition": partition, "device_groups": gd, "param_slices": gp,
-            "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L}
+            "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L,
+            "placement": placement}
     if route is not None:
         info["route"] = route.summary()
         info["route_digest"] = route.digest()

@@ -607,3 +607,26 @@ def test_mewma_tf1_zero_copy_equals_staged(gpu, monkeypatch, use_filtered, init,
         assert a.dtype == r.dtype and np.array_equal(a, r)
     for a, r in zip(s_got, s_ref):
         assert a.dtype == r.dtype and np.array_equal(a, r)
+
+
+@pytest.mark.parametrize("L,hl,hr,C", [(12, 4, 4, 3), (5, 1, 0, 2)])
+def test_placement_calibrated_shard_round_equals_oracle(gpu, L, hl, hr, C):
+    """A shard whose stacks were chosen by the placement probe (federated_amd/placement.py) mixes
+    exactly as the oracle says: the probe changes where the buckets live, not the round; its
+    report names one chosen input and one chosen output stack among the candidates."""
+    from federated_amd.population import make_ring_shard
+    P = 70_001
+    shard, info = make_ring_shard(0, 1, L, hl, hr, P, torch.device("cuda"), None, gpu, placement_candidates=C)
+    rep = info["placement"]
+    assert rep["candidates"] == C and len(rep["in_us"]) == C and len(rep["out_us"]) == C
+    assert all(0 <= k < C for k in rep["chosen"]) and all(t > 0 for t in rep["in_us"] + rep["out_us"])
+    gen = torch.Generator(device="cuda")
+    for i in range(L):
+        gen.manual_seed(7 + i)
+        shard.models[i].normal_(generator=gen)
+    shard.round()
+    torch.cuda.synchronize()
+    host, mixed = shard.models.cpu().numpy(), shard.mixed.cpu().numpy()
+    for i in range(L):
+        ref = sequential_mix(host[i], [host[j] for j in shard.plan.neighbours(i)], shard.alphas)
+        assert np.array_equal(mixed[i], ref), i

@@ -1,0 +1,91 @@
+"""Host logic of the placement-calibrated stacks (federated_amd/placement.py): probe rows, the
+choice rule, and that calibrated_stacks keeps the fastest input stack, then the fastest output
+stack with it (stub engine and timer on CPU tensors)."""
+import os
+import sys
+
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from federated_amd import placement  # noqa: E402
+from federated_amd.population import make_ring_shard  # noqa: E402
+
+
+def test_probe_rows_spread_and_small_stacks():
+    assert placement.probe_rows(128, 8) == [0, 16, 32, 48, 64, 80, 96, 112]
+    assert placement.probe_rows(5, 8) == [0, 1, 2, 3, 4]
+    assert placement.probe_rows(9, 8) == sorted(set(placement.probe_rows(9, 8)))
+
+
+def test_choose_takes_the_smallest_median_first_on_ties():
+    assert placement.choose([[5, 5, 9], [4, 4, 6], [7, 1, 7]]) == 1
+    assert placement.choose([[3.0], [3.0]]) == 0
+
+
+class StubEngine:
+    """prepare_mix_seq returns a launch tagged with the (local, out) stacks it touches."""
+
+    def __init__(self):
+        self.calls = []
+
+    def prepare_mix_seq(self, out, local, nbrs, alphas):
+        assert len(nbrs) == len(alphas)
+
+        def launch(stream=None):
+            pass
+
+        launch.tag = (local.untyped_storage().data_ptr(), out.untyped_storage().data_ptr())
+        return launch
+
+
+@pytest.mark.parametrize("slow_in,slow_out", [({0: 9.0, 2: 7.0}, {1: 8.0}), ({}, {0: 3.0, 3: 3.0})])
+def test_calibrated_stacks_keep_the_fastest_input_then_output(monkeypatch, slow_in, slow_out):
+    C, L, P = 4, 6, 32
+    made = []
+    real_empty = torch.empty
+
+    def tracking_empty(*a, **k):
+        t = real_empty(*a, **k)
+        made.append(t)
+        return t
+
+    monkeypatch.setattr(placement.torch, "empty", tracking_empty)
+    cost = {}
+
+    def timer(fns):
+        ins = [t.untyped_storage().data_ptr() for t in made[:C]]
+        outs = [t.untyped_storage().data_ptr() for t in made[C:2 * C]]
+        i_ptr, o_ptr = fns[0].tag
+        i, o = ins.index(i_ptr), outs.index(o_ptr)
+        return len(fns) * 1e-6 * (1.0 + slow_in.get(i, 0.0) + slow_out.get(o, 0.0))
+
+    models, mixed, rep = placement.calibrated_stacks(L, P, "cpu", StubEngine(), 2, 2, candidates=C, rows=3,
+                                                     timer=timer)
+    a = min(range(C), key=lambda i: (slow_in.get(i, 0.0), i))
+    b = min(range(C), key=lambda j: (slow_out.get(j, 0.0), j))
+    assert rep["chosen"] == [a, b]
+    assert models.untyped_storage().data_ptr() == made[a].untyped_storage().data_ptr()
+    assert mixed.untyped_storage().data_ptr() == made[C + b].untyped_storage().data_ptr()
+    assert tuple(models.shape) == (L, P) and tuple(mixed.shape) == (L, P)
+    assert len(rep["in_us"]) == C and len(rep["out_us"]) == C and rep["probe_rows"] == 3
+    assert bool(torch.all(models == 0))  # probed on finite values
+
+
+def test_one_candidate_is_a_plain_allocation():
+    m, o, rep = placement.calibrated_stacks(3, 8, "cpu", None, 1, 1, candidates=1)
+    assert rep == {"candidates": 1} and tuple(m.shape) == (3, 8) and tuple(o.shape) == (3, 8)
+
+
+def test_ring_shard_takes_caller_stacks_and_checks_them():
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    plan = RingShardPlan(0, 1, 4, 1)
+    m, o = torch.zeros(4, 16), torch.zeros(4, 16)
+    shard = RingPopulationShard(plan, 16, "cpu", stacks=(m, o))
+    assert shard.models is m and shard.mixed is o
+    with pytest.raises(ValueError):
+        RingPopulationShard(plan, 16, "cpu", stacks=(torch.zeros(3, 16), o))
+    # on CPU (no HIP engine) make_ring_shard skips the calibration and says so
+    _, info = make_ring_shard(0, 1, 4, 1, 1, 16, "cpu", placement_candidates=4)
+    assert info["placement"] is None
