@@ -17,6 +17,10 @@ interior mixes, each boundary device mixing as soon as the rows it reads have la
 ``--partition hybrid --device-groups G`` combines the two. ``--devices-per-gpu L`` keeps the
 per-GPU population fixed instead (weak scaling, D = L*N).
 
+Each rank's population stacks are placement-calibrated before the timed region
+(``--placement-candidates``, federated_amd/placement.py: the fastest of 4 allocations per stack,
+probed with the same mix; the probe is reported in ``config.placement``).
+
 value = algorithmic bytes of all mixes on all ranks / max-over-ranks wall time, with
 algorithmic bytes = (K + 2) * P * 4 per device mix (K neighbour reads + local read + output
 write). Inputs are resident in HBM when the timed region starts.
