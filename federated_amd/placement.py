@@ -12,9 +12,9 @@ aligned addresses all spread over the same levels (``tools/alloc_experiment.py``
 A population lives for the whole run, so it can afford to choose: ``calibrated_stacks`` allocates
 ``candidates`` input stacks and as many output stacks (HBM holds them: the bench population is
 26 GB of 288), times the population's own ring-window mix on a spread of rows of each, keeps the
-fastest input stack, then the fastest output stack with it, and frees the others. The probe runs
-the production kernel on the stacks as they will be used; it changes where the buckets live, not
-what is computed."""
+fastest output stack (against the first input), then the fastest input stack with it, then the
+output again with that input, and frees the others. The probe runs the production kernel on the
+stacks as they will be used; it changes where the buckets live, not what is computed."""
 from __future__ import annotations
 
 import statistics
@@ -40,9 +40,10 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
                       rows: int = 8, passes: int = 3, dtype=torch.float32,
                       timer: Optional[Callable] = None) -> Tuple[torch.Tensor, torch.Tensor, dict]:
     """(models, mixed, report): two ``[L, P]`` stacks chosen among ``candidates`` allocations each
-    by timing the ring-window sequential mix (``hl`` below, ``hr`` above, wrap-around within the
-    stack) of ``rows`` spread rows. ``report`` holds every candidate's median microseconds per mix
-    and the chosen indices. ``timer(fns) -> seconds`` replaces the HIP-event timing (tests)."""
+    (output, then input, then output again) by timing the ring-window sequential mix (``hl``
+    below, ``hr`` above, wrap-around within the stack) of ``rows`` spread rows. ``report`` holds
+    every candidate's median microseconds per mix and the chosen indices. ``timer(fns) ->
+    seconds`` replaces the HIP-event timing (tests)."""
     if candidates < 1:
         raise ValueError("need at least one candidate")
     dev = torch.device(device)
@@ -80,15 +81,20 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
 
     for m in ins:  # finite values: the probe's arithmetic must not depend on stale memory
         m.zero_()
-    t_in = measure([plan(m, outs[0]) for m in ins])
+    # coordinate descent: a slow stack on one side masks the other side's differences, so the
+    # output is chosen against input 0, the input against that output, then the output again
+    t_out0 = measure([plan(ins[0], o) for o in outs])
+    b = choose(t_out0)
+    t_in = measure([plan(m, outs[b]) for m in ins])
     a = choose(t_in)
-    t_out = measure([plan(ins[a], o) for o in outs])
+    t_out = measure([plan(ins[a], o) for o in outs]) if a != 0 else t_out0
     b = choose(t_out)
     models, mixed = ins[a], outs[b]
     del ins, outs
     if dev.type == "cuda":
         torch.cuda.empty_cache()
     report = {"candidates": candidates, "probe_rows": len(sel),
+              "out_us_vs_in0": [round(statistics.median(t), 2) for t in t_out0],
               "in_us": [round(statistics.median(t), 2) for t in t_in],
               "out_us": [round(statistics.median(t), 2) for t in t_out], "chosen": [a, b]}
     return models, mixed, report
