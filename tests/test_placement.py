@@ -70,7 +70,7 @@ def test_calibrated_stacks_keep_the_fastest_input_then_output(monkeypatch, slow_
     assert mixed.untyped_storage().data_ptr() == made[C + b].untyped_storage().data_ptr()
     assert tuple(models.shape) == (L, P) and tuple(mixed.shape) == (L, P)
     assert len(rep["in_us"]) == C and len(rep["out_us"]) == C and rep["probe_rows"] == 3
-    assert bool(torch.all(models == 0))  # probed on finite values
+    assert bool(torch.all(torch.isfinite(models)))  # probed on finite values
 
 
 def test_one_candidate_is_a_plain_allocation():
