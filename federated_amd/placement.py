@@ -51,8 +51,17 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
     if candidates < 1:
         raise ValueError("need at least one candidate")
     dev = torch.device(device)
-    ins = [torch.empty((L, P), dtype=dtype, device=dev) for _ in range(candidates)]
-    outs = [torch.empty((L, P), dtype=dtype, device=dev) for _ in range(candidates)]
+    ins, outs = [], []
+    for c in range(candidates):  # as many pairs as fit: never fail where a plain allocation would not
+        try:
+            pair = (torch.empty((L, P), dtype=dtype, device=dev), torch.empty((L, P), dtype=dtype, device=dev))
+        except torch.OutOfMemoryError:
+            if not ins:
+                raise
+            break
+        ins.append(pair[0])
+        outs.append(pair[1])
+    candidates = len(ins)
     if candidates == 1:
         return ins[0], outs[0], {"candidates": 1}
     K = hl + hr

@@ -55,8 +55,8 @@ def test_calibrated_stacks_keep_the_fastest_input_then_output(monkeypatch, slow_
     cost = {}
 
     def timer(fns):
-        ins = [t.untyped_storage().data_ptr() for t in made[:C]]
-        outs = [t.untyped_storage().data_ptr() for t in made[C:2 * C]]
+        ins = [t.untyped_storage().data_ptr() for t in made[0:2 * C:2]]  # allocated in (input, output) pairs
+        outs = [t.untyped_storage().data_ptr() for t in made[1:2 * C:2]]
         i_ptr, o_ptr = fns[0].tag
         i, o = ins.index(i_ptr), outs.index(o_ptr)
         return len(fns) * 1e-6 * (1.0 + slow_in.get(i, 0.0) + slow_out.get(o, 0.0))
@@ -66,8 +66,8 @@ def test_calibrated_stacks_keep_the_fastest_input_then_output(monkeypatch, slow_
     a = min(range(C), key=lambda i: (slow_in.get(i, 0.0), i))
     b = min(range(C), key=lambda j: (slow_out.get(j, 0.0), j))
     assert rep["chosen"] == [a, b]
-    assert models.untyped_storage().data_ptr() == made[a].untyped_storage().data_ptr()
-    assert mixed.untyped_storage().data_ptr() == made[C + b].untyped_storage().data_ptr()
+    assert models.untyped_storage().data_ptr() == made[2 * a].untyped_storage().data_ptr()
+    assert mixed.untyped_storage().data_ptr() == made[2 * b + 1].untyped_storage().data_ptr()
     assert tuple(models.shape) == (L, P) and tuple(mixed.shape) == (L, P)
     assert len(rep["in_us"]) == C and len(rep["out_us"]) == C and rep["probe_rows"] == 3
     assert bool(torch.all(torch.isfinite(models)))  # probed on finite values
@@ -89,3 +89,19 @@ def test_ring_shard_takes_caller_stacks_and_checks_them():
     # on CPU (no HIP engine) make_ring_shard skips the calibration and says so
     _, info = make_ring_shard(0, 1, 4, 1, 1, 16, "cpu", placement_candidates=4)
     assert info["placement"] is None
+
+
+def test_calibration_uses_the_pairs_that_fit(monkeypatch):
+    """Out of memory after two candidate pairs: the probe runs on those two instead of failing."""
+    real_empty, n = torch.empty, [0]
+
+    def limited_empty(*a, **k):
+        n[0] += 1
+        if n[0] > 4:
+            raise torch.OutOfMemoryError("stub: out of memory")
+        return real_empty(*a, **k)
+
+    monkeypatch.setattr(placement.torch, "empty", limited_empty)
+    m, o, rep = placement.calibrated_stacks(4, 16, "cpu", StubEngine(), 1, 1, candidates=4, rows=2,
+                                            timer=lambda fns: 1e-6 * len(fns))
+    assert rep["candidates"] == 2 and rep["chosen"] == [0, 0] and tuple(m.shape) == (4, 16)
