@@ -36,7 +36,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ballast-gib", type=int, default=0,
+                    help="hold this much device memory (touched) for the whole run before any bucket is "
+                         "allocated, so the buckets do not land on a process's first-allocation memory "
+                         "(the slow placement level, DESIGN §3)")
     a = ap.parse_args()
+    ballast = None
+    if a.ballast_gib:
+        ballast = torch.empty(a.ballast_gib << 28, dtype=torch.float32, device="cuda")
+        ballast.zero_()
     from federated_amd import _lib
     from federated_amd.engine import get_engine
     eng = get_engine(0)
