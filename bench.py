@@ -45,6 +45,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 KERNEL = "mix_vec_kernel"
+SCRUB_BYTES_PER_S = 20e9  # a conservative rate for the background scrub of freed device memory
 
 
 def parse():
@@ -473,6 +474,7 @@ def main():
         t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
         autotune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
                     "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
+        freed = 2 * shard.models.numel() * shard.models.element_size()  # the losing plan's two stacks
         if t_dir < t_rel:  # same decision on every rank: both times are maxima over ranks
             shard, info = dshard, dinfo
             autotune["chosen"] = "direct"
@@ -480,6 +482,9 @@ def main():
             del dshard
             autotune["chosen"] = "relayed"
         torch.cuda.empty_cache()
+        # freed device memory is scrubbed in the background at roughly 25-30 GB/s and slows the
+        # mixes while that runs (federated_amd/placement.py): let it finish before timing
+        time.sleep(freed / SCRUB_BYTES_PER_S + 0.1)
     watchdog.enter("timed rounds")
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
