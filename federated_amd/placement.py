@@ -50,6 +50,8 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
     seconds; ``report["settle"]``)."""
     if candidates < 1:
         raise ValueError("need at least one candidate")
+    if candidates > 1 and engine is None:
+        raise ValueError("the placement probe needs an engine (the mix it times)")
     dev = torch.device(device)
     ins, outs = [], []
     for c in range(candidates):  # as many pairs as fit: never fail where a plain allocation would not

@@ -105,3 +105,8 @@ def test_calibration_uses_the_pairs_that_fit(monkeypatch):
     m, o, rep = placement.calibrated_stacks(4, 16, "cpu", StubEngine(), 1, 1, candidates=4, rows=2,
                                             timer=lambda fns: 1e-6 * len(fns))
     assert rep["candidates"] == 2 and rep["chosen"] == [0, 0] and tuple(m.shape) == (4, 16)
+
+
+def test_probe_without_engine_is_refused():
+    with pytest.raises(ValueError):
+        placement.calibrated_stacks(4, 16, "cpu", None, 1, 1, candidates=2)
