@@ -45,7 +45,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 KERNEL = "mix_vec_kernel"
-SCRUB_BYTES_PER_S = 20e9  # a conservative rate for the background scrub of freed device memory
 
 
 def parse():
@@ -99,6 +98,9 @@ def parse():
                    help="allocate each population stack this many times and keep the fastest, timed "
                         "with the population's own mix before the timed region (federated_amd/placement.py; "
                         "1 = plain allocation)")
+    p.add_argument("--placement-release", action="store_true",
+                   help="return the rejected placement candidates to the driver (then wait out its "
+                        "background scrub) instead of leaving them in torch's caching allocator")
     p.add_argument("--watchdog-seconds", type=float, default=900.0,
                    help="end the run with status 124 and the phase it was in if it has not finished "
                         "after this long (a collective that never completes; 0 = off)")
@@ -450,7 +452,8 @@ def main():
                                       eng, partition=partition, dev_groups=args.device_groups,
                                       relay=(not args.no_relay) if relay is None else relay,
                                       staged=not args.no_stages, window_batch=args.window_batch,
-                                      placement_candidates=args.placement_candidates)
+                                      placement_candidates=args.placement_candidates,
+                                      placement_release=args.placement_release)
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -461,6 +464,13 @@ def main():
         return shard, info
 
     watchdog.enter(f"build {args.partition} shard")
+    def drop_cached():
+        """Between legs: with --placement-release, return cached memory to the driver (each leg's
+        calibration then settles after its scrub); by default it stays in torch's cache for the
+        next leg, so no scrub runs under a timed leg."""
+        if args.placement_release:
+            torch.cuda.empty_cache()
+
     shard, info = build(args.partition)
     autotune = None
     if world > 1 and info.get("route", {}).get("relay") and not args.no_autotune:
@@ -474,17 +484,14 @@ def main():
         t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
         autotune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
                     "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
-        freed = 2 * shard.models.numel() * shard.models.element_size()  # the losing plan's two stacks
         if t_dir < t_rel:  # same decision on every rank: both times are maxima over ranks
             shard, info = dshard, dinfo
             autotune["chosen"] = "direct"
         else:
             del dshard
             autotune["chosen"] = "relayed"
-        torch.cuda.empty_cache()
-        # freed device memory is scrubbed in the background at roughly 25-30 GB/s and slows the
-        # mixes while that runs (federated_amd/placement.py): let it finish before timing
-        time.sleep(freed / SCRUB_BYTES_PER_S + 0.1)
+        # the losing plan's stacks stay in torch's cache: memory returned to the driver is scrubbed
+        # in the background, which would slow the timed rounds (federated_amd/placement.py)
     watchdog.enter("timed rounds")
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
@@ -499,7 +506,7 @@ def main():
     legs = {}
     if world > 1 and args.partition == "devices" and not args.no_params_leg:
         del shard
-        torch.cuda.empty_cache()
+        drop_cached()
         extra = [("params", None, "same population and steps, every rank holds a 1/N element slice of "
                                   "every bucket (SURVEY §8 e (1)); no exchange")]
         if world >= 4 and D % 2 == 0:
@@ -517,7 +524,7 @@ def main():
                 leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
             legs[part if groups is None else f"{part}{groups}"] = leg
             del xshard
-            torch.cuda.empty_cache()
+            drop_cached()
         if not args.no_weak_leg and not weak:
             # weak form for reference: the single-GPU population on every rank (D = 128 N), the
             # same routed halo now hidden under 120 interior mixes per rank
@@ -529,7 +536,7 @@ def main():
                             "ms_per_step": round(wel / args.steps * 1e3, 4), "devices_total": Dw,
                             "note": f"{args.devices} devices per GPU (population grown with N), devices partition"}
             del wshard
-            torch.cuda.empty_cache()
+            drop_cached()
 
     result = None
     if rank == 0:

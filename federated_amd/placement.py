@@ -13,7 +13,9 @@ A population lives for the whole run, so it can afford to choose: ``calibrated_s
 ``candidates`` input stacks and as many output stacks (HBM holds them: the bench population is
 26 GB of 288), times the population's own ring-window mix on a spread of rows of each, keeps the
 fastest output stack (against the first input), then the fastest input stack with it, then the
-output again with that input, and frees the others. The probe runs the production kernel on the
+output again with that input, and drops the others into torch's caching allocator (returning
+them to the driver is an option: the driver's background scrub of freed memory then costs a
+settle period). The probe runs the production kernel on the
 stacks as they will be used; it changes where the buckets live, not what is computed."""
 from __future__ import annotations
 
@@ -39,14 +41,17 @@ def choose(times: Sequence[Sequence[float]]) -> int:
 def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidates: int = 4,
                       rows: int = 128, passes: int = 3, dtype=torch.float32,
                       timer: Optional[Callable] = None, hold: Optional[list] = None,
-                      settle_s: float = 8.0) -> Tuple[torch.Tensor, torch.Tensor, dict]:
+                      settle_s: float = 8.0, release: bool = False) -> Tuple[torch.Tensor, torch.Tensor, dict]:
     """(models, mixed, report): two ``[L, P]`` stacks chosen among ``candidates`` allocations each
     (output, then input, then output again) by timing the ring-window sequential mix (``hl``
     below, ``hr`` above, wrap-around within the stack) of ``rows`` spread rows. ``report`` holds
     every candidate's median microseconds per mix and the chosen indices. ``timer(fns) ->
     seconds`` replaces the HIP-event timing (tests). ``hold``: a list that receives the rejected
-    candidates instead of freeing them (measurement of their effect). After the rejects are
-    freed, mixes run on the chosen pair until their rate has settled (at most ``settle_s``
+    candidates instead of dropping them (measurement of their effect). Dropped candidates stay in
+    torch's caching allocator, reusable by the process's later allocations, as any freed tensor
+    does. ``release=True`` returns them to the driver instead (``torch.cuda.empty_cache``); the
+    driver then scrubs that memory in the background, which slows every mix by 1-3% for a few
+    seconds, so mixes run on the chosen pair until their rate has settled (at most ``settle_s``
     seconds; ``report["settle"]``)."""
     if candidates < 1:
         raise ValueError("need at least one candidate")
@@ -111,7 +116,7 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
         hold.extend(t for j, t in enumerate(outs) if j != b)
     del ins, outs
     settle = None
-    if dev.type == "cuda":
+    if dev.type == "cuda" and release:
         torch.cuda.empty_cache()
         if timer is None and settle_s > 0:
             target = statistics.median(t_out[b])

@@ -323,7 +323,8 @@ class RingPopulationShard:
 def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: int, device,
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
-                    window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0):
+                    window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
+                    placement_release: bool = False):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -351,7 +352,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":
         from .placement import calibrated_stacks
         models, mixed, placement = calibrated_stacks(L, Pr, device, engine, hl, hr, placement_candidates,
-                                                     dtype=dtype)
+                                                     dtype=dtype, release=placement_release)
         stacks = (models, mixed)
     shard = RingPopulationShard(plan, Pr, device, transport, engine, dtype, window_batch, route=route, rank=rank,
                                 stacks=stacks)
