@@ -61,11 +61,21 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // Explicit per-call configurations go through cfa_mix_seq_ex_f32.
 // Defaults from the in-process sweep on MI355X (tools/tune_mix.py, profiles/r01_tune.jsonl):
 // 2 resident workgroups per CU with a grid-stride loop, nontemporal loads and stores, and
-// vec_per_lane = 0 (auto: the widest tile that keeps (n+1)*vec <= 40 float4 in registers).
+// vec_per_lane = 0 (auto: the widest tile that keeps (n+1)*vec <= 40 float4 in registers); the
+// streaming mix kernel has its own default below.
+// blocks_per_cu = kAutoBlocks in the library default means "per kernel": the streaming mix
+// kernel takes its own shape (mix_auto_shape), every other kernel kDefaultBlocks.
+constexpr int kDefaultBlocks = 2;
+constexpr int kAutoBlocks = -1;
 static int norm_vec(int v) { return v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0)); }
 static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ? 2 : 1); }
+// The streaming mix's own default (round 2, tools/probe/tune_placed.py on placement-calibrated
+// stacks, profiles/r02_tune_placed.jsonl: every shape of 1-4 workgroups per CU x 1/2/4 float4 per
+// lane at K = 2/4/8/12 on two boxes): one workgroup per CU (one wave per SIMD) at every fan-in,
+// two float4 per lane except for 3-5 neighbours, where one is best.
+static int mix_auto_vec(int n) { return (n >= 3 && n <= 5) ? 1 : ((n + 1) * 2 <= 40 ? 2 : 1); }
 static cfa_launch_t read_tune() {
-  cfa_launch_t t{2, 0, 1};
+  cfa_launch_t t{kAutoBlocks, 0, 1};
   if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
   if (const char* s = getenv("CFA_VEC_PER_LANE")) t.vec_per_lane = norm_vec(atoi(s));
   if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
@@ -105,8 +115,9 @@ namespace {
 static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
   if (tiles <= 0) return 1;
   long long g = tiles;
-  if (t.blocks_per_cu > 0) {
-    long long cap = (long long)device_cus() * t.blocks_per_cu;
+  const int bpc = t.blocks_per_cu == kAutoBlocks ? kDefaultBlocks : t.blocks_per_cu;
+  if (bpc > 0) {
+    long long cap = (long long)device_cus() * bpc;
     if (g > cap) g = cap;
   }
   if (g > 0x7fffffffLL) g = 0x7fffffffLL;

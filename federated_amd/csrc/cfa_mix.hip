@@ -246,10 +246,15 @@ static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, 
                              const cfa_launch_t& t) {
   // the divisor fold carries a guarded division per element and step: one float4 per lane
   // keeps more tiles in flight per VGPR budget (tools/probe/div_sweep.py: 6.03 vs 5.69 TB/s)
+  // library default (blocks_per_cu == kAutoBlocks): the mix's own shape, one workgroup per CU;
+  // an explicit configuration (cfa_mix_seq_ex_f32, CFA_BLOCKS_PER_CU) keeps the round-1 auto vec
+  const bool own = t.blocks_per_cu == kAutoBlocks && RULE != CFA_RULE_SEQUENTIAL_DIV;
   const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane)
-                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : auto_vec(n));
+                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : (own ? mix_auto_vec(n) : auto_vec(n)));
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
-  const unsigned grid = grid_for(tiles, t);
+  cfa_launch_t shape = t;
+  if (own) shape.blocks_per_cu = 1;
+  const unsigned grid = grid_for(tiles, shape);
   if (U == 4) {
     if (t.nontemporal) launch_vec_u<RULE, 4, true>(n, grid, st, out, f, nvec);
     else launch_vec_u<RULE, 4, false>(n, grid, st, out, f, nvec);
@@ -391,8 +396,8 @@ extern "C" int cfa_mix_seq_ex_f32(float* out, const float* local, const float* c
                                   const float* alphas, int n, size_t P,
                                   const cfa_launch_t* launch, void* stream) {
   if (n > 0 && !alphas) return fail(CFA_E_INVALID, "null alphas");
+  if (launch && launch->blocks_per_cu < 0) return fail(CFA_E_INVALID, "blocks_per_cu < 0");
   cfa_launch_t lc = launch ? *launch : tune();
-  if (lc.blocks_per_cu < 0) return fail(CFA_E_INVALID, "blocks_per_cu < 0");
   lc.vec_per_lane = norm_vec(lc.vec_per_lane);
   return mix_seq_any(out, local, nbrs, alphas, n, P, nullptr, (hipStream_t)stream, lc);
 }
