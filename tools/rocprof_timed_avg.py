@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, required=True)
-    ap.add_argument("--kernel", default="mix_vec_kernel<8, 0, 4, true>")
+    ap.add_argument("--kernel", default="mix_vec_kernel<8, 0, 2, true>")
     a = ap.parse_args()
     with open(a.trace) as fh:
         rows = [r for r in csv.DictReader(fh) if a.kernel in r["Kernel_Name"]]
