@@ -3,6 +3,15 @@
 // row of a ring window once for up to 8 consecutive devices.
 #include "cfa_internal.h"
 
+// Resident workgroups per CU across a whole population launch (all devices together). 8 by
+// default; CFA_POP_WG_PER_CU overrides it per call (read at each launch, so one process can
+// compare values: tools/probe/pop_shape.py).
+static int pop_wg_per_cu() {
+  const char* s = getenv("CFA_POP_WG_PER_CU");
+  const int v = s ? atoi(s) : 0;
+  return v > 0 ? v : 8;
+}
+
 namespace {
 
 // ------------------------------------------------------------------------------------------
@@ -435,7 +444,7 @@ extern "C" int cfa_mix_population_tf1_f32(float* const* out_ptrs, const float* c
   if (D > 65535) return fail(CFA_E_INVALID, "D=%d exceeds grid.y limit", D);
   const long long nvec = (long long)P / 4;
   long long gx = (nvec + kBlock - 1) / kBlock;
-  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  const long long cap = ((long long)device_cus() * pop_wg_per_cu() + D - 1) / D;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   population_tf1_kernel<<<dim3((unsigned)gx, (unsigned)D), kBlock, 0, (hipStream_t)stream>>>(
@@ -459,7 +468,7 @@ extern "C" int cfa_mix_population_f32(float* const* out_ptrs, const float* const
   // host layer); the body runs on float4, the <4-element tail in the first tile column.
   const long long nvec = (long long)P / 4;
   long long gx = (nvec + 2LL * kBlock - 1) / (2LL * kBlock);
-  const long long cap = ((long long)device_cus() * 8 + D - 1) / D;
+  const long long cap = ((long long)device_cus() * pop_wg_per_cu() + D - 1) / D;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, (unsigned)D);
@@ -582,7 +591,7 @@ extern "C" int cfa_ge_population_step_f32(float* const* out_ptrs, const float* c
   // buckets are 16-byte aligned (allocator contract, checked by the host layer)
   const long long nvec = (long long)P / 4;
   long long gx = (nvec + kBlock - 1) / kBlock;
-  const long long cap = ((long long)device_cus() * 8 + D + reduce_M - 1) / (D + reduce_M);
+  const long long cap = ((long long)device_cus() * pop_wg_per_cu() + D + reduce_M - 1) / (D + reduce_M);
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, (unsigned)(D + reduce_M));
