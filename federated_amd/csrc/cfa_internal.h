@@ -83,6 +83,14 @@ static cfa_launch_t read_tune() {
 }
 static const cfa_launch_t& tune() {
   static const cfa_launch_t t = read_tune();  // C++11 magic static: thread-safe init
+  // CFA_TUNE_DYNAMIC=1 (measurement tools only): re-read the environment at every launch, so one
+  // process can compare launch shapes on the same buffers (tools/probe/tune_entries.py)
+  static const bool dynamic = getenv("CFA_TUNE_DYNAMIC") != nullptr;
+  if (dynamic) {
+    thread_local cfa_launch_t d;
+    d = read_tune();
+    return d;
+  }
   return t;
 }
 
@@ -122,6 +130,14 @@ static unsigned grid_for(long long tiles, const cfa_launch_t& t = tune()) {
   }
   if (g > 0x7fffffffLL) g = 0x7fffffffLL;
   return (unsigned)g;
+}
+
+// grid_for with a kernel's own default workgroups per CU, used while the launch configuration is
+// the library default (an explicit CFA_BLOCKS_PER_CU applies to every kernel alike).
+static unsigned grid_for_own(long long tiles, int own_blocks_per_cu) {
+  cfa_launch_t t = tune();
+  if (t.blocks_per_cu == kAutoBlocks) t.blocks_per_cu = own_blocks_per_cu;
+  return grid_for(tiles, t);
 }
 
 // Kernel-argument pack: pointers + coefficients land in SGPRs.

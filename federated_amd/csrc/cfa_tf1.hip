@@ -380,7 +380,10 @@ static int tf1_pass(void* out, int out_mode, const float* local, const double* w
   };
   if (nvec > 0) {
     const Tf1Fanin f = fanin_at(head);
-    const unsigned grid = grid_for(((long long)nvec + kBlock - 1) / kBlock);
+    // the fp64-output (wide) form runs one workgroup per CU: 0.749 against 0.729 of peak on the
+    // same buffers (tools/kernel_rooflines.py --bpc-variants 2,1); the fp32 outputs keep two
+    const long long vt = ((long long)nvec + kBlock - 1) / kBlock;
+    const unsigned grid = out_mode == kOutF64 ? grid_for_own(vt, 1) : grid_for(vt);
     const CompressParams c = shifted(head);
     void* o = out_at(head);
     const long long nv = (long long)nvec;
@@ -635,7 +638,8 @@ extern "C" int cfa_mewma_tf1_f64(double* W, double* const* s, const double* cons
       vec = vec && a.gstride[j] == 1 && (addr(a.s[j]) & 15) == 0 && (addr(a.g[j]) & 15) == 0;
     const long long nvec2 = vec ? (long long)P / 2 : 0;
     if (nvec2 > 0) {
-      launch_mewma_f64_vec(m, grid_for((nvec2 + kBlock - 1) / kBlock), st, a, nvec2,
+      // one workgroup per CU: 0.733 against 0.714 of peak on the same buffers (--bpc-variants 2,1)
+      launch_mewma_f64_vec(m, grid_for_own((nvec2 + kBlock - 1) / kBlock, 1), st, a, nvec2,
                            std::make_integer_sequence<int, CFA_MAX_FANIN>{});
       if (int rc = check_launch("mewma_tf1_f64_vec")) return rc;
     }

@@ -19,7 +19,10 @@ import torch  # noqa: E402
 PEAK = 8000.0
 
 
-def timed(fn, reps, warm=3):
+BPC_VARIANTS = []  # --bpc-variants: workgroups per CU compared on the same buffers (CFA_TUNE_DYNAMIC)
+
+
+def _timed_once(fn, reps, warm):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -32,6 +35,21 @@ def timed(fn, reps, warm=3):
     return a.elapsed_time(b) / reps  # ms
 
 
+def timed(fn, reps, warm=3):
+    """ms per launch; with --bpc-variants a dict {workgroups per CU: ms}, the variants
+    interleaved over three passes on the same buffers (median per variant)."""
+    if not BPC_VARIANTS:
+        return _timed_once(fn, reps, warm)
+    import statistics
+    t = {v: [] for v in BPC_VARIANTS}
+    for _ in range(3):
+        for v in BPC_VARIANTS:
+            os.environ["CFA_BLOCKS_PER_CU"] = str(v)
+            t[v].append(_timed_once(fn, reps, warm))
+    os.environ.pop("CFA_BLOCKS_PER_CU", None)
+    return {v: statistics.median(x) for v, x in t.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--params", type=int, default=25_000_000)
@@ -40,7 +58,13 @@ def main():
                     help="hold this much device memory (touched) for the whole run before any bucket is "
                          "allocated, so the buckets do not land on a process's first-allocation memory "
                          "(the slow placement level, DESIGN §3)")
+    ap.add_argument("--bpc-variants", default="",
+                    help="comma list of workgroups per CU to compare on the same buffers, e.g. 2,1 "
+                         "(sets CFA_TUNE_DYNAMIC before the library loads)")
     a = ap.parse_args()
+    if a.bpc_variants:
+        os.environ["CFA_TUNE_DYNAMIC"] = "1"
+        BPC_VARIANTS.extend(int(v) for v in a.bpc_variants.split(","))
     ballast = None
     if a.ballast_gib:
         ballast = torch.empty(a.ballast_gib << 28, dtype=torch.float32, device="cuda")
@@ -55,6 +79,10 @@ def main():
     rows = []
 
     def rec(name, entry, bytes_, ms, note=""):
+        if isinstance(ms, dict):
+            for v, m in ms.items():
+                rec(name, entry, bytes_, m, (note + "; " if note else "") + f"blocks_per_cu={v}")
+            return
         gbs = bytes_ / (ms * 1e-3) / 1e9
         r = {"kernel_entry": entry, "case": name, "params": P, "avg_launch_ms": round(ms, 4),
              "algorithmic_bytes": bytes_, "GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
