@@ -72,7 +72,7 @@ static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ?
 // The streaming mix's own default (round 2, tools/probe/tune_placed.py on placement-calibrated
 // stacks, profiles/r02_tune_placed.jsonl: every shape of 1-4 workgroups per CU x 1/2/4 float4 per
 // lane at K = 2/4/8/12 on two boxes): one workgroup per CU (one wave per SIMD) at every fan-in,
-// two float4 per lane except for 3-5 neighbours, where one is best.
+// two float4 per lane except for 3-5 neighbours, where one is best. Sequential rule only.
 static int mix_auto_vec(int n) { return (n >= 3 && n <= 5) ? 1 : ((n + 1) * 2 <= 40 ? 2 : 1); }
 static cfa_launch_t read_tune() {
   cfa_launch_t t{kAutoBlocks, 0, 1};

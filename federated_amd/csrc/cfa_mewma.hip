@@ -118,7 +118,9 @@ extern "C" int cfa_mewma_update_f32(float* W, float* const* s, const float* cons
     if (vec) {
       const long long nvec = (long long)P / 4;
       if (nvec > 0) {
-        launch_mewma_vec(m, grid_for((nvec + kBlock - 1) / kBlock), st, a, nvec,
+        // one workgroup per CU: 0.792 against 0.778 of peak on the same buffers
+        // (tools/kernel_rooflines.py --bpc-variants)
+        launch_mewma_vec(m, grid_for_own((nvec + kBlock - 1) / kBlock, 1), st, a, nvec,
                          std::make_integer_sequence<int, CFA_MAX_FANIN>{});
         if (int rc = check_launch("mewma_vec")) return rc;
       }

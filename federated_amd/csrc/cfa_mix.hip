@@ -248,7 +248,9 @@ static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, 
   // keeps more tiles in flight per VGPR budget (tools/probe/div_sweep.py: 6.03 vs 5.69 TB/s)
   // library default (blocks_per_cu == kAutoBlocks): the mix's own shape, one workgroup per CU;
   // an explicit configuration (cfa_mix_seq_ex_f32, CFA_BLOCKS_PER_CU) keeps the round-1 auto vec
-  const bool own = t.blocks_per_cu == kAutoBlocks && RULE != CFA_RULE_SEQUENTIAL_DIV;
+  // (the sequential rule only: the linear closed form measured 0.752 with it against 0.790 with
+  // two workgroups x 4 float4 on the same buffers, profiles/r02_s3_kernel_rooflines_vec_same.jsonl)
+  const bool own = t.blocks_per_cu == kAutoBlocks && RULE == CFA_RULE_SEQUENTIAL;
   const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane)
                                    : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : (own ? mix_auto_vec(n) : auto_vec(n)));
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);

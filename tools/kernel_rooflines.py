@@ -43,10 +43,16 @@ def timed(fn, reps, warm=3):
     import statistics
     t = {v: [] for v in BPC_VARIANTS}
     for _ in range(3):
-        for v in BPC_VARIANTS:
-            os.environ["CFA_BLOCKS_PER_CU"] = str(v)
+        for v in BPC_VARIANTS:  # "B" = workgroups per CU, "B:V" = also float4 per lane
+            b, _, vec = str(v).partition(":")
+            os.environ["CFA_BLOCKS_PER_CU"] = b
+            if vec:
+                os.environ["CFA_VEC_PER_LANE"] = vec
+            else:
+                os.environ.pop("CFA_VEC_PER_LANE", None)
             t[v].append(_timed_once(fn, reps, warm))
     os.environ.pop("CFA_BLOCKS_PER_CU", None)
+    os.environ.pop("CFA_VEC_PER_LANE", None)
     return {v: statistics.median(x) for v, x in t.items()}
 
 
@@ -59,12 +65,13 @@ def main():
                          "allocated, so the buckets do not land on a process's first-allocation memory "
                          "(the slow placement level, DESIGN §3)")
     ap.add_argument("--bpc-variants", default="",
-                    help="comma list of workgroups per CU to compare on the same buffers, e.g. 2,1 "
+                    help="comma list of workgroups per CU (optionally :float4 per lane) to compare on the "
+                         "same buffers, e.g. 2,1 or 1:2,1:4 "
                          "(sets CFA_TUNE_DYNAMIC before the library loads)")
     a = ap.parse_args()
     if a.bpc_variants:
         os.environ["CFA_TUNE_DYNAMIC"] = "1"
-        BPC_VARIANTS.extend(int(v) for v in a.bpc_variants.split(","))
+        BPC_VARIANTS.extend(a.bpc_variants.split(","))
     ballast = None
     if a.ballast_gib:
         ballast = torch.empty(a.ballast_gib << 28, dtype=torch.float32, device="cuda")
