@@ -96,11 +96,24 @@ class GraphPopulationShard:
     """Device-resident buckets of one shard, its halo buffers, CSR tables and the round."""
 
     def __init__(self, plan: GraphShardPlan, P: int, device, transport=None, engine=None,
-                 policy: Callable = T.alphas_tf2, dtype=torch.float32):
+                 policy: Callable = T.alphas_tf2, dtype=torch.float32, placement_candidates: int = 0):
+        """``placement_candidates`` > 1: the models / mixed stacks are placement-calibrated
+        (``placement.calibrated_stacks``, probed with ring-window mixes of the same shapes; the
+        level is a property of the allocation, not of the topology) when the round runs
+        per-device streaming mixes (P above POPULATION_LAUNCH_MAX_P); ``self.placement`` holds
+        the probe."""
         self.plan, self.P = plan, int(P)
         self.device = torch.device(device)
-        self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
-        self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
+        self.placement = None
+        if (placement_candidates > 1 and engine is not None and self.device.type == "cuda"
+                and self.P > POPULATION_LAUNCH_MAX_P):
+            from .placement import calibrated_stacks
+            h = min(4, max(1, (plan.L - 1) // 2))
+            self.models, self.mixed, self.placement = calibrated_stacks(
+                plan.L, self.P, self.device, engine, h, h, placement_candidates, dtype=dtype)
+        else:
+            self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
+            self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
         self.halo = torch.empty((len(plan.halo_devices), self.P), dtype=dtype, device=self.device)
         self.transport, self.engine = transport, engine
         self.alphas = [list(policy(plan.lists[plan.first + i], plan.first + i, plan.D)) for i in range(plan.L)]

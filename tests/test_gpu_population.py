@@ -195,8 +195,8 @@ def test_config5_ring_round_world1(gpu):
         assert np.array_equal(out[i], sequential_mix(h[i], [h[(i - 1) % 128]], [0.5]))
 
 
-@pytest.mark.parametrize("P", [24_622, 2_100_003])  # one population launch / per-device streaming mixes
-def test_graph_population_round_world1(gpu, P):
+@pytest.mark.parametrize("P,placed", [(24_622, 0), (2_100_003, 0), (2_100_003, 2)])  # one population launch /
+def test_graph_population_round_world1(gpu, P, placed):                         # per-device streaming mixes
     """Arbitrary topology (vGraph rows with the random.choices draw) as one shard: the round
     equals per-device sequential mixes on the oracle, bit for bit."""
     import random as _random
@@ -209,7 +209,8 @@ def test_graph_population_round_world1(gpu, P):
     np.fill_diagonal(g, 0)
     lists = T.mobile(g[:, :, None], 0, 3, rng=_random.Random(3))
     plan = GraphShardPlan(lists, 0, 1)
-    shard = GraphPopulationShard(plan, P, torch.device("cuda"), None, gpu)
+    shard = GraphPopulationShard(plan, P, torch.device("cuda"), None, gpu, placement_candidates=placed)
+    assert (shard.placement is not None) == bool(placed)
     shard.models.normal_()
     shard.round()
     torch.cuda.synchronize()
