@@ -41,7 +41,8 @@ def choose(times: Sequence[Sequence[float]]) -> int:
 def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidates: int = 4,
                       rows: int = 128, passes: int = 3, dtype=torch.float32,
                       timer: Optional[Callable] = None, hold: Optional[list] = None,
-                      settle_s: float = 8.0, release: bool = False) -> Tuple[torch.Tensor, torch.Tensor, dict]:
+                      settle_s: float = 8.0, release: bool = False,
+                      min_alloc_bytes: int = 16 << 30) -> Tuple[torch.Tensor, torch.Tensor, dict]:
     """(models, mixed, report): two ``[L, P]`` stacks chosen among ``candidates`` allocations each
     (output, then input, then output again) by timing the ring-window sequential mix (``hl``
     below, ``hr`` above, wrap-around within the stack) of ``rows`` spread rows. ``report`` holds
@@ -52,16 +53,27 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
     does. ``release=True`` returns them to the driver instead (``torch.cuda.empty_cache``); the
     driver then scrubs that memory in the background, which slows every mix by 1-3% for a few
     seconds, so mixes run on the chosen pair until their rate has settled (at most ``settle_s``
-    seconds; ``report["settle"]``)."""
+    seconds; ``report["settle"]``). Each candidate stack is carved from an allocation of at
+    least ``min_alloc_bytes`` (device stacks of 1 GiB or more): a 16-device ring mixed from 16-, 32- or 64-row
+    allocations ran at 161-164 us, from the first 16 rows of a 128-row (12.8 GB) allocation at
+    154 us, in either allocation order (tools/probe/alloc_size.py)."""
     if candidates < 1:
         raise ValueError("need at least one candidate")
     if candidates > 1 and engine is None:
         raise ValueError("the placement probe needs an engine (the mix it times)")
     dev = torch.device(device)
     ins, outs = [], []
+    esize = dtype.itemsize
+    big = dev.type == "cuda" and L * P * esize >= (1 << 30)  # streaming-bound stacks only
+    floor = max(L * P, (min_alloc_bytes // esize) if big else 0)
+
+    def stack():
+        base = torch.empty(floor, dtype=dtype, device=dev)
+        return base[:L * P].view(L, P)
+
     for c in range(candidates):  # as many pairs as fit: never fail where a plain allocation would not
         try:
-            pair = (torch.empty((L, P), dtype=dtype, device=dev), torch.empty((L, P), dtype=dtype, device=dev))
+            pair = (stack(), stack())
         except torch.OutOfMemoryError:
             if not ins:
                 raise
