@@ -7,7 +7,9 @@ mixes read, or of the stack they write (``tools/probe/placement_pairs.py``). No 
 controls it: torch's allocator, hipExtMalloc default / contiguous / fine-grained / uncached, and
 virtual-memory mappings backed by 2 MiB, 64 MiB, 1 GiB or whole-range physical handles at 1 GiB
 aligned addresses all spread over the same levels (``tools/alloc_experiment.py``,
-``tools/probe/vmm_placement.py``).
+``tools/probe/vmm_placement.py``). Large allocations tend to the fast level
+(``tools/probe/alloc_size.py``), so candidate stacks are carved from allocations of 16 GiB or
+more.
 
 A population lives for the whole run, so it can afford to choose: ``calibrated_stacks`` allocates
 ``candidates`` input stacks and as many output stacks (HBM holds them: the bench population is
@@ -15,8 +17,8 @@ A population lives for the whole run, so it can afford to choose: ``calibrated_s
 fastest output stack (against the first input), then the fastest input stack with it, then the
 output again with that input, and drops the others into torch's caching allocator (returning
 them to the driver is an option: the driver's background scrub of freed memory then costs a
-settle period). The probe runs the production kernel on the
-stacks as they will be used; it changes where the buckets live, not what is computed."""
+settle period). The probe runs the production kernel on the stacks as they will be used; it
+changes where the buckets live, not what is computed."""
 from __future__ import annotations
 
 import statistics
