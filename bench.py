@@ -290,7 +290,10 @@ def open_transport(kind, rank, world, device, allow_fallback=False):
     """The requested transport, opened collectively: every rank takes the same decision (MIN over
     the gloo control group), so no rank is left waiting. If it cannot be opened the bench fails
     (TransportError on every rank) unless ``allow_fallback``: then torch.distributed P2P over an
-    nccl (= RCCL) group, then over the gloo group (host-staged). Returns (transport, comparable)."""
+    nccl (= RCCL) group, then over the gloo group (host-staged). Returns (transport, comparable):
+    a line is comparable only on a device-direct transport that was opened as requested (RCCL, or
+    ``--transport torch`` on an nccl group); ``--transport torch`` on the default gloo group stages
+    every exchange through host memory and is marked non-comparable, named ``torch-gloo``."""
     import torch.distributed as dist
     from federated_amd.dist import TorchTransport, make_transport
     import torch
@@ -307,7 +310,10 @@ def open_transport(kind, rank, world, device, allow_fallback=False):
         ok, err = 0, str(exc)
         print(f"[bench rank {rank}] {kind} transport failed ({exc})", file=sys.stderr)
     if agree(ok):
-        return t, True
+        staged = bool(getattr(t, "host_staged", False))
+        if staged and t.name == "torch":
+            t.name = "torch-gloo"
+        return t, not staged
     if t is not None:
         t.close()
     if not allow_fallback:
@@ -603,6 +609,15 @@ def main():
                     shard_P(info, P), K, kernel, args.window_batch or 1),
             },
         }
+        pl = info.get("placement") or {}
+        if pl.get("plain_us"):
+            # the same mix on candidate pair (0, 0), the first allocation of each stack: what the
+            # population runs at without the placement choice (probe timing, HIP events)
+            rl = result["roofline"]
+            plain = (K + 2) * shard_P(info, P) * 4 / (pl["plain_us"] * 1e-6) / 1e9
+            rl["achieved_plain_alloc"] = round(plain, 1)
+            rl["frac_plain_alloc"] = round(plain / HBM_PEAK_GBS, 4)
+            rl["placement_rejected_cached_GiB"] = pl.get("rejected_cached_GiB")
         if legs:
             result["partitions"] = legs
     if world > 1:

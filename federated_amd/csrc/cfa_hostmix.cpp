@@ -21,17 +21,13 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
-#include <mutex>
-#include <thread>
 #include <vector>
 
+#include "cfa_copypool.h"
 #include "cfa_engine.h"
 
 extern "C" void cfa_internal_set_error(const char* msg);
@@ -49,90 +45,14 @@ int hfail(int code, const char* fmt, ...) {
   return code;
 }
 
-struct Copy {
-  void* dst;
-  const void* src;
-  size_t bytes;
-};
+using cfa::Copy;
 
-// Fork-join pool of host threads for memcpy lists. One run at a time: a caller that finds the
-// pool busy (another thread's call) copies on its own thread instead of waiting. Workers spin
-// for a short while after each run before parking on the condition variable, so the runs of one
-// pipelined call (one per chunk, tens of microseconds apart) do not pay a futex wake-up each.
-class CopyPool {
- public:
-  static CopyPool& get() {
-    static CopyPool* pool = new CopyPool();  // never destroyed: workers may outlive static teardown
-    return *pool;
-  }
-
-  void run(const std::vector<Copy>& jobs, int threads) {
-    if (jobs.empty()) return;
-    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-    const int want = std::min<int>(threads, int(jobs.size()));
-    if (!busy.owns_lock() || want <= 1) {
-      for (const Copy& c : jobs) memcpy(c.dst, c.src, c.bytes);
-      return;
-    }
-    ensure(want - 1);
-    jobs_ = &jobs;
-    next_.store(0, std::memory_order_relaxed);
-    helpers_.store(want - 1, std::memory_order_relaxed);
-    pending_.store(want - 1, std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> g(mu_);  // under the lock: a parking worker cannot miss it
-      gen_.fetch_add(1, std::memory_order_release);
-    }
-    cv_.notify_all();
-    drain();
-    for (long spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin)
-      if (spin > 4096) std::this_thread::yield();
-    jobs_ = nullptr;
-  }
-
- private:
-  void ensure(int n) {
-    std::lock_guard<std::mutex> g(mu_);
-    while (int(workers_.size()) < n) {
-      const int id = int(workers_.size());
-      workers_.emplace_back([this, id] { loop(id); });
-      workers_.back().detach();
-    }
-  }
-
-  void drain() {
-    const std::vector<Copy>& jobs = *jobs_;
-    for (size_t i = next_.fetch_add(1); i < jobs.size(); i = next_.fetch_add(1))
-      memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
-  }
-
-  void loop(int id) {
-    uint64_t seen = 0;
-    for (;;) {
-      auto t0 = std::chrono::steady_clock::now();
-      for (long spin = 0; gen_.load(std::memory_order_acquire) == seen; ++spin) {
-        if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
-          std::unique_lock<std::mutex> g(mu_);
-          cv_.wait(g, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-          break;
-        }
-        __builtin_ia32_pause();
-      }
-      seen = gen_.load(std::memory_order_acquire);
-      if (id >= helpers_.load(std::memory_order_relaxed)) continue;  // not needed for this run
-      drain();
-      pending_.fetch_sub(1, std::memory_order_acq_rel);
-    }
-  }
-
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_;
-  std::vector<std::thread> workers_;
-  const std::vector<Copy>* jobs_ = nullptr;
-  std::atomic<size_t> next_{0};
-  std::atomic<int> helpers_{0}, pending_{0};
-  std::atomic<uint64_t> gen_{0};
-};
+// The process-wide copy pool (cfa_copypool.h: one atomic (generation, helpers) word per run,
+// bounded wait). Never destroyed: its workers may outlive static teardown.
+cfa::CopyPool& copy_pool() {
+  static cfa::CopyPool* pool = new cfa::CopyPool();
+  return *pool;
+}
 
 constexpr size_t kPiece = size_t(256) << 10;  // bytes per copy job (load balance across threads)
 
@@ -181,7 +101,7 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t step = pad4(std::max<size_t>(chunk_elems, 4));
   const int nthreads = std::max(1, std::min(threads, 64));
-  CopyPool& pool = CopyPool::get();
+  cfa::CopyPool& pool = copy_pool();
 
   struct Chunk {
     size_t a, b, off;
@@ -204,12 +124,17 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
   size_t launched = 0, unpacked = 0;
   std::vector<Copy> jobs;
   std::vector<const float*> nb(size_t(std::max(n, 1)));
-  auto unpack = [&](size_t c) {
+  auto copy_all = [&](const char* what, size_t c) -> int {
+    if (pool.run(jobs.data(), jobs.size(), nthreads)) return CFA_OK;
+    return hfail(CFA_E_HIP, "hostmix: host copy pool did not finish the %s of chunk %zu (pool disabled; "
+                 "later calls copy on the calling thread)", what, c);
+  };
+  auto unpack = [&](size_t c) -> int {
     jobs.clear();
     for_pieces(chunks[c].a, chunks[c].b, [&](int k, size_t x, size_t y) {
       add_copies(jobs, out_layers[k] + (x - lo[size_t(k)]), out_pinned + x, (y - x) * sizeof(float));
     });
-    pool.run(jobs, nthreads);
+    return copy_all("unpack", c);
   };
   for (size_t c = 0; c < chunks.size() && rc == CFA_OK; ++c) {
     Chunk& ch = chunks[c];
@@ -221,7 +146,7 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
         add_copies(jobs, row + (x - ch.a), in_layers[size_t(m) * L + k] + (x - lo[size_t(k)]), (y - x) * sizeof(float));
       });
     }
-    pool.run(jobs, nthreads);
+    if ((rc = copy_all("pack", c)) != CFA_OK) break;
     float* ds = static_cast<float*>(dstage) + ch.off;
     for (int j = 0; j < n; ++j) nb[size_t(j)] = ds + size_t(j + 1) * w;
     float* dst = static_cast<float*>(dout) + ch.a;
@@ -234,7 +159,7 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
     }
     ++launched;
     // unpack whatever earlier chunks have finished while this one is in flight
-    while (unpacked < c && hipEventQuery(chunks[unpacked].ev) == hipSuccess) unpack(unpacked++);
+    while (rc == CFA_OK && unpacked < c && hipEventQuery(chunks[unpacked].ev) == hipSuccess) rc = unpack(unpacked++);
   }
   if (rc == CFA_OK) {
     for (; unpacked < launched; ++unpacked) {
@@ -242,7 +167,7 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
         rc = hfail(CFA_E_HIP, "hostmix: chunk %zu failed", unpacked);
         break;
       }
-      unpack(unpacked);
+      if ((rc = unpack(unpacked)) != CFA_OK) break;
     }
   }
   if (rc != CFA_OK) (void)hipStreamSynchronize(st);  // drain: no kernel may still read the staging

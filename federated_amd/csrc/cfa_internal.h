@@ -76,7 +76,10 @@ static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ?
 static int mix_auto_vec(int n) { return (n >= 3 && n <= 5) ? 1 : ((n + 1) * 2 <= 40 ? 2 : 1); }
 static cfa_launch_t read_tune() {
   cfa_launch_t t{kAutoBlocks, 0, 1};
-  if (const char* s = getenv("CFA_BLOCKS_PER_CU")) t.blocks_per_cu = atoi(s);
+  if (const char* s = getenv("CFA_BLOCKS_PER_CU")) {
+    const int v = atoi(s);  // 0 = one workgroup per tile, > 0 = cap per CU; negative = the default
+    t.blocks_per_cu = v >= 0 ? v : kAutoBlocks;
+  }
   if (const char* s = getenv("CFA_VEC_PER_LANE")) t.vec_per_lane = norm_vec(atoi(s));
   if (const char* s = getenv("CFA_NONTEMPORAL")) t.nontemporal = atoi(s) ? 1 : 0;
   return t;

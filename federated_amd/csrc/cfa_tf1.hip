@@ -433,6 +433,15 @@ int mix_tf1_impl(void* out, bool out64, const float* local, const float* const* 
   if (out64 && n == 0) return fail(CFA_E_INVALID, "%s: needs at least one neighbour", fn);
   // null pointers, and an output that starts at a neighbour bucket (fp32 or fp64 alike)
   if (int rc = validate_mix(static_cast<const float*>(out), local, nbrs, n, P)) return rc;
+  if (out64 && P > 0) {
+    // an fp64 out is 8P bytes: each lane's store would overwrite fp32 inputs other lanes have not
+    // read yet, so it must not overlap any input range at all (local included)
+    const uintptr_t o0 = addr(out), o1 = o0 + P * sizeof(double);
+    auto overlaps = [&](const float* x) { return addr(x) < o1 && o0 < addr(x) + P * sizeof(float); };
+    if (overlaps(local)) return fail(CFA_E_INVALID, "%s: fp64 out overlaps local", fn);
+    for (int j = 0; j < n; ++j)
+      if (overlaps(nbrs[j])) return fail(CFA_E_INVALID, "%s: fp64 out overlaps neighbour %d", fn, j);
+  }
   CompressParams cp{};
   if (int rc = compress_params(mode, cp)) return rc;
   cp.cbegin = (long long)cbegin;

@@ -34,6 +34,12 @@ class TorchTransport:
     def __init__(self, group=None):
         self.group = group
 
+    @property
+    def host_staged(self) -> bool:
+        """True on a gloo group: device buffers go through host memory, so an exchange measured on
+        this transport says nothing about xGMI (a bench line on it is not comparable)."""
+        return dist.get_backend(self.group) == "gloo"
+
     def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
         """Grouped exchange. gloo moves host tensors only, so device buffers are staged through
         host memory (synchronously); with nccl the ops are issued on ``stream``."""
@@ -86,6 +92,7 @@ class RcclTransport:
     """RCCL communicator from libcfa.so (one per process/GPU)."""
 
     name = "rccl"
+    host_staged = False
 
     def __init__(self, rank: int, world: int, device: int, group=None):
         from . import _lib

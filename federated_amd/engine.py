@@ -10,6 +10,8 @@ reference's per-layer arrays to and from that flat form.
 """
 from __future__ import annotations
 
+import contextlib
+
 import ctypes
 from typing import Iterable, Optional, Sequence
 
@@ -262,16 +264,19 @@ class Engine:
         if len(alphas) != len(nbrs):
             raise ValueError("one alpha per neighbour required")
         # above CFA_MAX_FANIN the passes chain through an fp64 scratch bucket from torch's
-        # allocator (stream-ordered, and capturable), not a library allocation
-        scratch = (torch.empty(P, dtype=torch.float64, device=self.device)
-                   if len(nbrs) > _lib.CFA_MAX_FANIN else None)
+        # allocator (stream-ordered, and capturable), not a library allocation. It is allocated
+        # on the stream the kernel writes it on: a block from another stream's pool could still
+        # be in use by work queued there.
+        scratch = None
+        if len(nbrs) > _lib.CFA_MAX_FANIN:
+            ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+            with ctx:
+                scratch = torch.empty(P, dtype=torch.float64, device=self.device)
         _lib.call("cfa_mix_tf1_ex_f32", out.data_ptr(), local.data_ptr(),
                   _lib.ptr_table([x.data_ptr() for x in nbrs]), _lib.double_array(alphas),
                   len(nbrs), P, int(mode), int(cbegin), int(cend),
                   kept.data_ptr() if kept is not None else None,
                   scratch.data_ptr() if scratch is not None else None, self.stream_handle(stream))
-        if scratch is not None and stream is not None:
-            scratch.record_stream(stream)
         return out
 
     def mix_tf1_f64(self, out: torch.Tensor, local: torch.Tensor, nbrs: Sequence[torch.Tensor],

@@ -286,14 +286,14 @@ class RoutedExchange:
 
 
 def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world: int = 1,
-                   lo: int = 0, hi: Optional[int] = None, slice_bounds: Optional[Sequence[int]] = None
-                   ) -> List[Transfer]:
+                   slice_bounds: Optional[Sequence[int]] = None) -> List[Transfer]:
     """Global transfer list of a ring-window population in contiguous device blocks.
 
     Device block d (of ``dev_world``) sends its last ``hl`` rows to block d + 1's left halo and its
     first ``hr`` rows to block d - 1's right halo. With ``slice_world`` > 1 (hybrid partition)
     each block is held by ``slice_world`` ranks, rank = d * slice_world + p, each holding element
-    slice p of every bucket (``slice_bounds``), and transfers stay within a slice.
+    slice p of every bucket (``slice_bounds``), and transfers stay within a slice. Element ranges
+    are in the rank's own buffer coordinates: [0, slice length) of its slice, [0, P) without one.
 
     Stages: the left-halo row nearest the block (device first - 1, read by all hl left boundary
     devices) travels in stage 0, the farthest (device first - hl, read only by device 0) in stage
@@ -304,10 +304,7 @@ def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world
     for d in range(dev_world):
         left, right = (d - 1) % dev_world, (d + 1) % dev_world
         for p in range(slice_world):
-            if slice_bounds is not None:
-                a, b = slice_bounds[p], slice_bounds[p + 1]
-            else:
-                a, b = lo, (P if hi is None else hi)
+            a, b = (slice_bounds[p], slice_bounds[p + 1]) if slice_bounds is not None else (0, P)
             me = d * slice_world + p
             for q in range(hl):
                 out.append(Transfer(hl - 1 - q, left * slice_world + p, me, ("models", L - hl + q),

@@ -40,11 +40,18 @@ def choose(times: Sequence[Sequence[float]]) -> int:
     return min(range(len(med)), key=lambda i: (med[i], i))
 
 
+def fit_candidates(candidates: int, stack_bytes: int, free_bytes: int, budget_frac: float) -> int:
+    """How many (input, output) candidate pairs of ``stack_bytes`` allocations the probe may hold
+    at once within ``budget_frac`` of ``free_bytes`` (at least one: the plain allocation)."""
+    return max(1, min(int(candidates), int(budget_frac * free_bytes) // max(1, 2 * int(stack_bytes))))
+
+
 def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidates: int = 4,
                       rows: int = 128, passes: int = 3, dtype=torch.float32,
                       timer: Optional[Callable] = None, hold: Optional[list] = None,
                       settle_s: float = 8.0, release: bool = False,
-                      min_alloc_bytes: int = 16 << 30) -> Tuple[torch.Tensor, torch.Tensor, dict]:
+                      min_alloc_bytes: int = 16 << 30, budget_frac: float = 0.6
+                      ) -> Tuple[torch.Tensor, torch.Tensor, dict]:
     """(models, mixed, report): two ``[L, P]`` stacks chosen among ``candidates`` allocations each
     (output, then input, then output again) by timing the ring-window sequential mix (``hl``
     below, ``hr`` above, wrap-around within the stack) of ``rows`` spread rows. ``report`` holds
@@ -58,7 +65,15 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
     seconds; ``report["settle"]``). Each candidate stack is carved from an allocation of at
     least ``min_alloc_bytes`` (device stacks of 1 GiB or more): a 16-device ring mixed from 16-, 32- or 64-row
     allocations ran at 161-164 us, from the first 16 rows of a 128-row (12.8 GB) allocation at
-    154 us, in either allocation order (tools/probe/alloc_size.py)."""
+    154 us, in either allocation order (tools/probe/alloc_size.py).
+
+    Footprint: the probe holds 2 x ``candidates`` such allocations at once, so ``candidates`` is
+    capped to what fits in ``budget_frac`` of the device's free memory at entry. The chosen pair
+    keeps its whole allocations alive (the placement is a property of the allocation). The report
+    states the allocation size, the bytes the chosen pair holds, the bytes the rejected candidates
+    leave in torch's cache (0 with ``release``), and ``plain_us``: the probe time of candidate
+    pair (0, 0), the first allocation of each stack, i.e. what the population runs at without the
+    choice."""
     if candidates < 1:
         raise ValueError("need at least one candidate")
     if candidates > 1 and engine is None:
@@ -73,6 +88,12 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
         base = torch.empty(floor, dtype=dtype, device=dev)
         return base[:L * P].view(L, P)
 
+    capped = None
+    if dev.type == "cuda" and candidates > 1:
+        fit = fit_candidates(candidates, floor * esize, torch.cuda.mem_get_info(dev)[0], budget_frac)
+        if fit < candidates:
+            capped, candidates = candidates, fit
+
     for c in range(candidates):  # as many pairs as fit: never fail where a plain allocation would not
         try:
             pair = (stack(), stack())
@@ -83,8 +104,13 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
         ins.append(pair[0])
         outs.append(pair[1])
     candidates = len(ins)
+    gib = float(1 << 30)
+    footprint = {"alloc_GiB_per_stack": round(floor * esize / gib, 3),
+                 "data_GiB_per_stack": round(L * P * esize / gib, 3)}
+    if capped is not None:
+        footprint["candidates_capped_from"] = capped
     if candidates == 1:
-        return ins[0], outs[0], {"candidates": 1}
+        return ins[0], outs[0], {"candidates": 1, **footprint}
     K = hl + hr
     alphas = [1.0 / (K + 1)] * K
     offsets = [o for o in range(-hl, 0)] + [o for o in range(1, hr + 1)]
@@ -138,7 +164,12 @@ def calibrated_stacks(L: int, P: int, device, engine, hl: int, hr: int, candidat
     report = {"candidates": candidates, "probe_rows": len(sel),
               "out_us_vs_in0": [round(statistics.median(t), 2) for t in t_out0],
               "in_us": [round(statistics.median(t), 2) for t in t_in],
-              "out_us": [round(statistics.median(t), 2) for t in t_out], "chosen": [a, b]}
+              "out_us": [round(statistics.median(t), 2) for t in t_out], "chosen": [a, b],
+              "plain_us": round(statistics.median(t_out0[0]), 2),
+              "chosen_us": round(statistics.median(t_out[b]), 2),
+              **footprint,
+              "held_GiB": round(2 * floor * esize / gib, 3),
+              "rejected_cached_GiB": 0.0 if release else round((2 * candidates - 2) * floor * esize / gib, 3)}
     if settle is not None:
         report["settle"] = settle
     return models, mixed, report

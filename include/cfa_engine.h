@@ -18,7 +18,9 @@
  *     Every compute call is asynchronous on that stream.
  *   - Return 0 on success, a negative CFA_E* code on failure. `cfa_last_error()` returns a
  *     thread-local message for the last failure on the calling thread. No exceptions cross
- *     the ABI. The library keeps no global mutable state: calls are re-entrant.
+ *     the ABI. Calls are re-entrant and thread-safe. The one piece of process-wide state is the
+ *     host copy pool behind the host mix entry below, whose workers are created on first use and
+ *     never destroyed: one call owns it at a time, and a concurrent call copies on its own thread.
  *   - `P` is the bucket length in fp32 elements. A "bucket" is one model (or gradient)
  *     flattened layer by layer, in the order the reference passes its tensors.
  *   - Pointer arrays (`nbrs`, `alphas`, `coeff`, `s`, `g`) are HOST arrays whose entries are
@@ -292,7 +294,8 @@ CFA_API int cfa_mix_tf1_f32(float* out, const float* local, const float* const* 
  * fp64 arrays the reference itself returns when its inputs are fp32 (cfa.py:66-76 under numpy 2:
  * fp32 first subtraction, fp64 after; the epilogue in fp64). Equal to cfa_mix_tf1_f64 on the
  * widened buckets with step0_f32 = 1, at half the input bytes. n >= 1; passes above
- * CFA_MAX_FANIN chain in `out` itself (no scratch, no allocation). */
+ * CFA_MAX_FANIN chain in `out` itself (no scratch, no allocation). `out` (8 * P bytes) must not
+ * overlap `local` or any neighbour (CFA_E_INVALID). */
 CFA_API int cfa_mix_tf1_wide_f32(double* out, const float* local, const float* const* nbrs,
                                  const double* alphas, int n, size_t P, int mode, size_t cbegin,
                                  size_t cend, unsigned long long* kept_count, void* stream);

@@ -71,11 +71,27 @@ def test_calibrated_stacks_keep_the_fastest_input_then_output(monkeypatch, slow_
     assert tuple(models.shape) == (L, P) and tuple(mixed.shape) == (L, P)
     assert len(rep["in_us"]) == C and len(rep["out_us"]) == C and rep["probe_rows"] == 3
     assert bool(torch.all(torch.isfinite(models)))  # probed on finite values
+    # pair (0, 0) is the plain-allocation figure; the chosen pair's time is never above it
+    assert rep["plain_us"] == rep["out_us_vs_in0"][0]
+    assert rep["chosen_us"] <= rep["plain_us"]
+    gib = L * P * 4 / float(1 << 30)
+    assert rep["held_GiB"] == round(2 * gib, 3)
+    assert rep["rejected_cached_GiB"] == round((2 * C - 2) * gib, 3)
+
+
+def test_probe_footprint_is_capped_by_free_memory():
+    """The probe holds 2 x candidates allocations: never more than budget_frac of free memory."""
+    GiB = 1 << 30
+    assert placement.fit_candidates(4, 16 * GiB, 288 * GiB, 0.6) == 4   # the bench: 128 of 172 GiB
+    assert placement.fit_candidates(4, 16 * GiB, 100 * GiB, 0.6) == 1   # 60 GiB holds one pair
+    assert placement.fit_candidates(4, 16 * GiB, 120 * GiB, 0.6) == 2
+    assert placement.fit_candidates(4, 16 * GiB, 10 * GiB, 0.6) == 1    # never below the plain pair
 
 
 def test_one_candidate_is_a_plain_allocation():
     m, o, rep = placement.calibrated_stacks(3, 8, "cpu", None, 1, 1, candidates=1)
-    assert rep == {"candidates": 1} and tuple(m.shape) == (3, 8) and tuple(o.shape) == (3, 8)
+    assert rep["candidates"] == 1 and tuple(m.shape) == (3, 8) and tuple(o.shape) == (3, 8)
+    assert rep["data_GiB_per_stack"] == rep["alloc_GiB_per_stack"]  # host stacks: no floor
 
 
 def test_ring_shard_takes_caller_stacks_and_checks_them():
