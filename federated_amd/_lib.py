@@ -197,7 +197,7 @@ _exp = None
 
 
 def load_experiments() -> ctypes.CDLL:
-    """The measurement-only library of tools/ (csrc/cfa_experiments.hip); never used by the
+    """The measurement-only library of tools/ (tools/experiments/cfa_experiments.hip); never used by the
     product. Its entry points are bound by the tools themselves; errors via cfa_exp_last_error."""
     global _exp
     load()  # the HIP runtime torch loaded, as for libcfa

@@ -114,7 +114,12 @@ class GraphPopulationShard:
         else:
             self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
             self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
-        self.halo = torch.empty((len(plan.halo_devices), self.P), dtype=dtype, device=self.device)
+        carved = None
+        if self.placement is not None and plan.halo_devices:
+            from .placement import spare_view  # halo rows on the calibrated models allocation
+            carved = spare_view(self.models, [(len(plan.halo_devices), self.P)])
+        self.halo = carved[0] if carved is not None else torch.empty((len(plan.halo_devices), self.P), dtype=dtype,
+                                                                      device=self.device)
         self.transport, self.engine = transport, engine
         self.alphas = [list(policy(plan.lists[plan.first + i], plan.first + i, plan.D)) for i in range(plan.L)]
         self._tables = {}

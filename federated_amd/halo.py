@@ -255,11 +255,18 @@ class RoutedExchange:
     so the caller can record an event there and start that stage's boundary mixes."""
 
     def __init__(self, plan: RoutePlan, rank: int, buffers: Callable[[Hashable], "object"], transport,
-                 device=None, dtype=None):
+                 device=None, dtype=None, relay=None):
+        """``relay``: caller-provided staging of shape ``[2, >= slot_elems(rank)]`` (e.g. carved from
+        a calibrated allocation); allocated here when None."""
         import torch
         self.plan, self.rank, self.transport = plan, int(rank), transport
         n = plan.slot_elems(self.rank)
-        self.relay = torch.empty((2, max(n, 1)), dtype=dtype or torch.float32, device=device)
+        if relay is not None:
+            if relay.dim() != 2 or relay.shape[0] != 2 or relay.shape[1] < n:
+                raise ValueError(f"relay staging must be [2, >= {n}]")
+            self.relay = relay
+        else:
+            self.relay = torch.empty((2, max(n, 1)), dtype=dtype or torch.float32, device=device)
 
         def view(key, off, cnt):
             buf = self.relay[key[1]] if isinstance(key, tuple) and key and key[0] == "relay" else buffers(key)

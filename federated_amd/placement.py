@@ -40,6 +40,29 @@ def choose(times: Sequence[Sequence[float]]) -> int:
     return min(range(len(med)), key=lambda i: (med[i], i))
 
 
+def spare_view(stack: torch.Tensor, shapes, align: int = 64) -> Optional[List[torch.Tensor]]:
+    """Views of the given ``shapes`` carved, in order and ``align``-element aligned, from the part
+    of ``stack``'s allocation that lies past the stack itself (a calibrated stack is the head of
+    an allocation of 16 GiB or more, ``calibrated_stacks``), or None when the allocation has no
+    room. The shard's halo rows and relay slots live there, on the calibrated allocation instead
+    of small allocations of their own (which tend to land on the slower placement level)."""
+    st = stack.untyped_storage()
+    esize = stack.element_size()
+    total = st.nbytes() // esize
+    off = stack.storage_offset() + stack.numel()
+    views = []
+    for shape in shapes:
+        n = 1
+        for x in shape:
+            n *= int(x)
+        off = -(-off // align) * align
+        if off + n > total:
+            return None
+        views.append(torch.empty(0, dtype=stack.dtype, device=stack.device).set_(st, off, tuple(shape)))
+        off += n
+    return views
+
+
 def fit_candidates(candidates: int, stack_bytes: int, free_bytes: int, budget_frac: float) -> int:
     """How many (input, output) candidate pairs of ``stack_bytes`` allocations the probe may hold
     at once within ``budget_frac`` of ``free_bytes`` (at least one: the plain allocation)."""
@@ -192,3 +215,96 @@ def _settle(fns, run_time, target_us: float, max_s: float, window: int = 5, tol:
         if done or time.perf_counter() - t0 > max_s:
             return {"seconds": round(time.perf_counter() - t0, 2), "target_us": round(target_us, 2),
                     "window_medians_us": meds, "settled": bool(done)}
+
+
+def calibrated_rotation(count: int, L: int, P: int, device, engine, candidates: int = 6, hl: int = 2,
+                        hr: int = 2, rows: int = 64, passes: int = 3, dtype=torch.float32,
+                        timer: Optional[Callable] = None, min_alloc_bytes: int = 16 << 30,
+                        budget_frac: float = 0.6) -> Tuple[List[torch.Tensor], dict]:
+    """``count`` ``[L, P]`` stacks for a population whose rounds ROTATE its stacks through every
+    role (read as the current models, read as the previous round's published models, written as
+    the output: ``topology.Tf1PopulationRound``'s (current, previous, out), cfa.py:105-154), chosen
+    among ``candidates`` allocations (each carved from ``min_alloc_bytes`` or more, as in
+    ``calibrated_stacks``).
+
+    Every stack is both read and written over a rotation, so each candidate is scored by the sum
+    of two median probe times: written as the output of a ring-window sequential mix (``hl``
+    below, ``hr`` above) of ``rows`` spread rows whose inputs are two other candidates, and read as
+    the current models with the same two others as neighbours and output. The ``count`` lowest
+    scores are kept (ties to the earlier candidate); the rest go to torch's cache. Returns (stacks
+    in candidate order, report with every score and ``plain_us``: the score of candidates
+    0..count-1, the stacks a plain allocation gets)."""
+    if count < 1:
+        raise ValueError("need at least one stack")
+    dev = torch.device(device)
+    esize = dtype.itemsize
+    big = dev.type == "cuda" and L * P * esize >= (1 << 30)
+    floor = max(L * P, (min_alloc_bytes // esize) if big else 0)
+    if candidates > count and dev.type == "cuda":
+        fit = int(budget_frac * torch.cuda.mem_get_info(dev)[0]) // max(1, floor * esize)
+        candidates = max(count, min(candidates, fit))
+    if candidates <= count or L < 1:
+        stacks = [torch.zeros(L, P, dtype=dtype, device=dev) for _ in range(count)]
+        return stacks, {"candidates": count}
+    if engine is None:
+        raise ValueError("the placement probe needs an engine (the mix it times)")
+    cand = []
+    for _ in range(candidates):
+        try:
+            cand.append(torch.empty(floor, dtype=dtype, device=dev)[:L * P].view(L, P))
+        except torch.OutOfMemoryError:
+            break
+    if len(cand) <= count:
+        return cand[:count] + [torch.zeros(L, P, dtype=dtype, device=dev) for _ in range(count - len(cand))], \
+            {"candidates": len(cand)}
+    gen = torch.Generator(device=dev).manual_seed(20261015)
+    for c in cand:
+        c.normal_(generator=gen)
+    K = hl + hr
+    alphas = [1.0 / (K + 1)] * K
+    offsets = [o for o in range(-hl, 0)] + [o for o in range(1, hr + 1)]
+    sel = probe_rows(L, rows)
+
+    def plan(cur, prev, out):
+        return [engine.prepare_mix_seq(out[d], cur[d], [prev[(d + k) % L] for k in offsets], alphas) for d in sel]
+
+    def run_time(fns) -> float:
+        if timer is not None:
+            return timer(fns)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for fn in fns:
+            fn(None)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3
+
+    def others(c):
+        o = [i for i in range(len(cand)) if i != c]
+        return o[0], o[1]
+
+    plans = []
+    for c in range(len(cand)):
+        a, b = others(c)
+        plans.append(plan(cand[a], cand[b], cand[c]))  # c written
+        plans.append(plan(cand[c], cand[a], cand[b]))  # c read as the current models
+    for fns in plans:
+        run_time(fns)
+    t = [[] for _ in plans]
+    for _ in range(passes):
+        for i, fns in enumerate(plans):
+            t[i].append(run_time(fns) / len(fns) * 1e6)
+    out_us = [statistics.median(t[2 * c]) for c in range(len(cand))]
+    in_us = [statistics.median(t[2 * c + 1]) for c in range(len(cand))]
+    score = [o + i for o, i in zip(out_us, in_us)]
+    keep = sorted(sorted(range(len(cand)), key=lambda c: (score[c], c))[:count])
+    chosen = [cand[c] for c in keep]
+    del cand, plans
+    gib = float(1 << 30)
+    report = {"candidates": len(score), "probe_rows": len(sel), "out_us": [round(x, 2) for x in out_us],
+              "in_us": [round(x, 2) for x in in_us], "chosen": keep,
+              "plain_us": round(statistics.mean(score[:count]) / 2, 2),
+              "chosen_us": round(statistics.mean(score[c] for c in keep) / 2, 2),
+              "alloc_GiB_per_stack": round(floor * esize / gib, 3), "data_GiB_per_stack": round(L * P * esize / gib, 3),
+              "rejected_cached_GiB": round((len(score) - count) * floor * esize / gib, 3)}
+    return chosen, report

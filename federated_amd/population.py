@@ -141,7 +141,7 @@ class RingPopulationShard:
 
     def __init__(self, plan: RingShardPlan, P: int, device, transport=None, engine=None,
                  dtype=torch.float32, window_batch: int = 0, route=None, rank: Optional[int] = None,
-                 stacks: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+                 stacks: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, carve: bool = True):
         """``window_batch`` = B > 0 mixes B consecutive devices per ``cfa_mix_window_f32`` pass,
         loading each row of their shared window once (identical results); 0 = one streaming
         mix per device.
@@ -152,7 +152,10 @@ class RingPopulationShard:
         ``rank`` is this shard's global rank in that plan (default ``plan.rank``).
 
         ``stacks`` = (models, mixed): caller-allocated ``[L, P]`` stacks (e.g. placement-calibrated,
-        ``federated_amd.placement``) instead of fresh ones."""
+        ``federated_amd.placement``) instead of fresh ones. With ``carve`` the halo rows and the
+        relay slots are cut from the spare part of the models stack's allocation when it has room
+        (``placement.spare_view``: a calibrated stack heads an allocation of 16 GiB or more), so
+        they share its placement; otherwise they are allocated on their own."""
         if window_batch and not (1 <= window_batch <= 8 and plan.hl <= 4 and plan.hr <= 4):
             raise ValueError("window_batch must be 1..8 with at most 4 neighbours per side")
         self.window_batch = int(window_batch)
@@ -168,17 +171,28 @@ class RingPopulationShard:
         else:
             self.models = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
             self.mixed = torch.empty((plan.L, self.P), dtype=dtype, device=self.device)
-        self.halo = {
-            "left": torch.empty((plan.hl, self.P), dtype=dtype, device=self.device),
-            "right": torch.empty((plan.hr, self.P), dtype=dtype, device=self.device),
-        }
+        self.rank = plan.rank if rank is None else int(rank)
+        self.route = route  # as given (None: the direct plan below)
+        if route is None and plan.world > 1:
+            route = self._direct_route()
+        slot = route.slot_elems(self.rank) if route is not None else 0
+        carved = None
+        if stacks is not None and carve and plan.world > 1:
+            from .placement import spare_view
+            carved = spare_view(self.models, [(plan.hl, self.P), (plan.hr, self.P), (2, max(slot, 1))])
+        if carved is not None:
+            self.halo = {"left": carved[0], "right": carved[1]}
+            self._relay_buf = carved[2]
+        else:
+            self.halo = {
+                "left": torch.empty((plan.hl, self.P), dtype=dtype, device=self.device),
+                "right": torch.empty((plan.hr, self.P), dtype=dtype, device=self.device),
+            }
+            self._relay_buf = None
+        self.carved = carved is not None
         self.transport = transport
         self.engine = engine
         self.alphas = [1.0 / (plan.K + 1)] * plan.K
-        self.rank = plan.rank if rank is None else int(rank)
-        self.route = route
-        if route is None and plan.world > 1:
-            route = self._direct_route()
         self._route_plan = route
         self._routed = None
         self._launch = {}
@@ -221,7 +235,7 @@ class RingPopulationShard:
         if self._routed is None and self._route_plan is not None:
             from .halo import RoutedExchange
             self._routed = RoutedExchange(self._route_plan, self.rank, self.buffer, self.transport,
-                                          self.device, self.models.dtype)
+                                          self.device, self.models.dtype, relay=self._relay_buf)
         return self._routed
 
     def exchange(self, stream=None) -> None:

@@ -242,10 +242,21 @@ class Tf1PopulationRound:
     previous into out, then (current, previous, out) <- (out, current, previous). One
     ``cfa_mix_population_tf1_f32`` launch per round over the source table [current | previous]."""
 
-    def __init__(self, engine: Engine, D: int, P: int, device=None):
+    def __init__(self, engine: Engine, D: int, P: int, device=None, placement_candidates: int = 0):
+        """``placement_candidates`` > 3: the three stacks are placement-calibrated
+        (``placement.calibrated_rotation``: each stack is in turn read and written, so every
+        candidate is scored in both roles) when a stack is 1 GiB or more; ``self.placement``
+        holds the probe."""
         dev = engine.device if device is None else torch.device(device)
         self.engine, self.D, self.P = engine, int(D), int(P)
-        self._bufs = [torch.zeros(self.D, self.P, device=dev) for _ in range(3)]
+        self.placement = None
+        if placement_candidates > 3 and dev.type == "cuda" and self.D * self.P * 4 >= (1 << 30):
+            from .placement import calibrated_rotation
+            self._bufs, self.placement = calibrated_rotation(3, self.D, self.P, dev, engine, placement_candidates)
+            for b in self._bufs:
+                b.zero_()
+        else:
+            self._bufs = [torch.zeros(self.D, self.P, device=dev) for _ in range(3)]
         self._rot = 0
         self._tables = []
         for r in range(3):

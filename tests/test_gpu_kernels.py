@@ -566,6 +566,28 @@ def test_tf1_wide_equals_f64_rows(gpu, n, P, off, mode):
     assert int(kw.item()) == int(kf.item())
 
 
+@pytest.mark.parametrize("where", ["local", "nbr_tail", "nbr_head", "local_start"])
+def test_tf1_wide_rejects_fp64_out_overlapping_inputs(gpu, where):
+    """The fp64 out is 8P bytes: any overlap with an fp32 input range is refused before launch
+    (ADVICE r02), not only an out that starts at a neighbour."""
+    from federated_amd import _lib
+    P = 1024
+    buf = torch.zeros(8 * P, device="cuda")  # room for every layout below
+    local, nbr = buf[:P], buf[4 * P:5 * P]
+    base = buf.data_ptr()
+    out_ptr = {"local": base + 8,                       # inside local
+               "nbr_tail": base + 4 * P * 4 - 8 * P + 16,  # its tail reaches the neighbour
+               "nbr_head": base + 4 * P * 4 + 8,  # starts inside the neighbour
+               "local_start": base}[where]
+    with pytest.raises(_lib.CFAError, match="overlaps"):
+        _lib.call("cfa_mix_tf1_wide_f32", out_ptr, local.data_ptr(), _lib.ptr_table([nbr.data_ptr()]),
+                  _lib.double_array([0.5]), 1, P, 0, 0, 0, None, gpu.stream_handle())
+    ok = torch.empty(P, dtype=torch.float64, device="cuda")
+    _lib.call("cfa_mix_tf1_wide_f32", ok.data_ptr(), local.data_ptr(), _lib.ptr_table([nbr.data_ptr()]),
+              _lib.double_array([0.5]), 1, P, 0, 0, 0, None, gpu.stream_handle())
+    torch.cuda.synchronize()
+
+
 def test_full_size_tf1_wide_and_sharded_fedavg(gpu):
     """BASELINE size (8 neighbours x 25M): the TF1 wide kernel against the oracle's fp64 chain
     over the whole bucket, bit for bit (fp32 arrays in, the reference's fp64 result out), and

@@ -126,3 +126,80 @@ def test_calibration_uses_the_pairs_that_fit(monkeypatch):
 def test_probe_without_engine_is_refused():
     with pytest.raises(ValueError):
         placement.calibrated_stacks(4, 16, "cpu", None, 1, 1, candidates=2)
+
+
+def test_calibrated_rotation_drops_the_slow_candidates():
+    """Rotating stacks (Tf1PopulationRound): a candidate slow as output and as input is dropped;
+    the kept stacks are the lowest scores in candidate order."""
+    C, L, P = 6, 5, 16
+    slow = {1: 5.0, 4: 5.0}
+    made = []
+
+    class TagEngine(StubEngine):
+        def prepare_mix_seq(self, out, local, nbrs, alphas):
+            fn = super().prepare_mix_seq(out, local, nbrs, alphas)
+            made.append(fn)
+            return fn
+
+    stacks_holder = {}
+
+    def timer(fns):
+        ptrs = stacks_holder["ptrs"]
+        i_ptr, o_ptr = fns[0].tag
+        return len(fns) * 1e-6 * (1.0 + slow.get(ptrs.index(o_ptr), 0.0) + slow.get(ptrs.index(i_ptr), 0.0))
+
+    real_empty = torch.empty
+    allocs = []
+
+    def tracking_empty(*a, **k):
+        t = real_empty(*a, **k)
+        allocs.append(t)
+        stacks_holder["ptrs"] = [x.untyped_storage().data_ptr() for x in allocs]
+        return t
+
+    import unittest.mock as um
+    with um.patch.object(placement.torch, "empty", tracking_empty):
+        stacks, rep = placement.calibrated_rotation(3, L, P, "cpu", TagEngine(), candidates=C, rows=3, timer=timer)
+    assert rep["candidates"] == C and len(stacks) == 3
+    assert 1 not in rep["chosen"] and 4 not in rep["chosen"]
+    assert rep["chosen"] == sorted(rep["chosen"])
+    assert [s.untyped_storage().data_ptr() for s in stacks] == [stacks_holder["ptrs"][c] for c in rep["chosen"]]
+    assert all(tuple(s.shape) == (L, P) for s in stacks)
+    assert rep["chosen_us"] <= rep["plain_us"]
+
+
+def test_calibrated_rotation_plain_when_no_spare_candidates():
+    stacks, rep = placement.calibrated_rotation(3, 4, 8, "cpu", None, candidates=3)
+    assert rep == {"candidates": 3} and len(stacks) == 3 and all(float(s.abs().sum()) == 0 for s in stacks)
+
+
+def test_spare_view_carves_after_the_stack():
+    base = torch.arange(1000, dtype=torch.float32)
+    stack = base[:2 * 100].view(2, 100)
+    v = placement.spare_view(stack, [(3, 50), (2, 7)], align=64)
+    assert v is not None and tuple(v[0].shape) == (3, 50) and tuple(v[1].shape) == (2, 7)
+    assert v[0].storage_offset() == 256 and v[1].storage_offset() == 448  # 64-aligned after 200
+    assert float(v[0][0, 0]) == 256.0
+    v[1].fill_(-1)
+    assert float(base[448]) == -1 and float(base[461]) == -1 and float(base[462]) == 462
+    assert placement.spare_view(stack, [(9, 100)]) is None  # no room
+    assert placement.spare_view(torch.zeros(2, 100), [(1, 1)]) is None  # a plain stack has none
+
+
+def test_ring_shard_halo_and_relay_carved_from_calibrated_stacks():
+    """World 8 shard on caller stacks with spare room: halo rows and relay slots live in the
+    models allocation past the stack, and the routed exchange uses them."""
+    from federated_amd.halo import RoutePlan, ring_transfers
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    L, P, h, world, rank = 16, 4096, 4, 8, 3
+    plan = RingShardPlan(rank, world, L, h)
+    route = RoutePlan(world, ring_transfers(world, L, h, h, P))
+    big_m = torch.zeros(L * P + 2 * h * P + 2 * route.slot_elems(rank) + 1024)
+    m, o = big_m[:L * P].view(L, P), torch.zeros(L, P)
+    shard = RingPopulationShard(plan, P, "cpu", stacks=(m, o), route=route, rank=rank)
+    assert shard.carved
+    ptr0, ptr1 = big_m.data_ptr(), big_m.data_ptr() + big_m.numel() * 4
+    for t in (shard.halo["left"], shard.halo["right"], shard.routed().relay):
+        assert ptr0 + L * P * 4 <= t.data_ptr() < ptr1
+    plain = RingPopulationShard(plan, P, "cpu", stacks=(torch.zeros(L, P), o), route=route, rank=rank)
+    assert not plain.carved and plain.routed().relay.shape[0] == 2
