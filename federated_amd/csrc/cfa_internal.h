@@ -169,6 +169,32 @@ __device__ __forceinline__ float div_rn(float a, float b, float rb, bool fast) {
   return a / b;
 }
 
+// div_rn on the four lanes of a float4 with ONE range test for all four: the Markstein steps run
+// on every lane, and only when some |a| lies outside the guard (zeros, subnormals, huge values,
+// infinities) does the IEEE division redo the four lanes. max3/min3 of the magnitudes replace four
+// pairs of compares and four exec-mask branches. A NaN lane passes through either path as a NaN
+// (fmaxf/fminf skip it; Markstein on a NaN gives a NaN).
+__device__ __forceinline__ f4 div4_rn(f4 a, float b, float rb, bool fast) {
+  const float mx = fmaxf(fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)),
+                         fmaxf(__builtin_fabsf(a.z), __builtin_fabsf(a.w)));
+  const float mn = fminf(fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)),
+                         fminf(__builtin_fabsf(a.z), __builtin_fabsf(a.w)));
+  if (fast && mn >= 0x1p-100f && mx <= 0x1p100f) {
+    f4 q = a * rb;
+    f4 r;
+    r.x = __builtin_fmaf(-q.x, b, a.x);
+    r.y = __builtin_fmaf(-q.y, b, a.y);
+    r.z = __builtin_fmaf(-q.z, b, a.z);
+    r.w = __builtin_fmaf(-q.w, b, a.w);
+    q.x = __builtin_fmaf(r.x, rb, q.x);
+    q.y = __builtin_fmaf(r.y, rb, q.y);
+    q.z = __builtin_fmaf(r.z, rb, q.z);
+    q.w = __builtin_fmaf(r.w, rb, q.w);
+    return q;
+  }
+  return a / b;
+}
+
 // Host side: fills f.r / f.fast_div from f.d[0..n].
 inline void set_reciprocals(Fanin& f, int n) {
   bool fast = true;
@@ -210,10 +236,7 @@ __device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
     for (int j = 1; j <= N; ++j) {
       f4 t = v[j] - w;  // numpy: (x - w)
       t = f.c[j] * t;   //        u * (...)
-      t.x = div_rn(t.x, f.d[j], f.r[j], f.fast_div);  // (...) / C, IEEE-correct fp32 division
-      t.y = div_rn(t.y, f.d[j], f.r[j], f.fast_div);
-      t.z = div_rn(t.z, f.d[j], f.r[j], f.fast_div);
-      t.w = div_rn(t.w, f.d[j], f.r[j], f.fast_div);
+      t = div4_rn(t, f.d[j], f.r[j], f.fast_div);  // (...) / C, IEEE-correct fp32 division
       w = w + t;
     }
     return w;

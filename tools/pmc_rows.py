@@ -11,7 +11,8 @@ own (MI355X_MICROARCH.md §rocprofv3 PMC slots):
 Per kernel it reports HBM bytes per launch against the algorithmic bytes (traffic ratio: above
 1.0 = wasted re-reads), the share of wave time spent issuing VALU (SQ_ACTIVE_INST_VALU /
 SQ_WAVE_CYCLES) and parked on memory (SQ_WAIT_ANY / SQ_WAVE_CYCLES), VALU instructions per
-64 elements, and the child's event-timed launch time. The headline mix (cfa_mix_seq_f32, n = 8)
+64 elements, and GRBM busy cycles per XCD. Rates come from tools/kernel_rooflines.py: launches timed
+while counters are collected are not representative. The headline mix (cfa_mix_seq_f32, n = 8)
 is the calibration row: its traffic ratio is 1.0001x (profiles/r01_pmc_traffic.json).
 
 Usage: python tools/pmc_rows.py [--kernels a,b] [--out DIR]   (on the GPU box)
@@ -163,11 +164,10 @@ def main():
                 row["kernel"] = kname
                 vals.update(med)
                 row.setdefault("dispatches", {}).update(count)
-            if ms:
-                t = statistics.median(ms)
-                row["avg_launch_ms"] = round(t, 4)
-                row["GBps"] = round(alg(P) / (t * 1e-3) / 1e9, 1)
-                row["frac"] = round(row["GBps"] / PEAK, 4)
+            if ms:  # event time of the child's launches while counters were collected: not a rate
+                row["avg_launch_ms_under_pmc"] = round(statistics.median(ms), 4)
+            if "GRBM_GUI_ACTIVE" in vals:  # summed over the 8 XCDs: busy cycles of one launch
+                row["gui_active_cycles_per_xcd"] = round(vals["GRBM_GUI_ACTIVE"] / 8.0, 1)
             row["counters"] = vals
             if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
                 rd, wr = 2.0 * vals["FETCH_SIZE"] * 1024.0, vals["WRITE_SIZE"] * 1024.0
