@@ -282,9 +282,11 @@ __global__ __launch_bounds__(kBlock) void mewma_tf1_f64_kernel(MewmaF64Args a, l
 
 // Vector form for unit-stride, 16-byte-aligned buckets: two doubles per lane, the fan-in N at
 // compile time so that every W / g / s load is issued before the first update.
-template <int N>
+// ANY32 = false is the all-fp64 case (mask 0, what the TF1 drivers hold after loadmat / np.zeros):
+// the dtype flags are then compile-time false and the per-product fp32 selects disappear.
+template <int N, bool ANY32>
 __global__ __launch_bounds__(kBlock) void mewma_tf1_f64_vec_kernel(MewmaF64Args a, long long nvec2) {
-  const bool s32 = a.mask & CFA_TF1_STATE_F32, g32 = a.mask & CFA_TF1_GRAD_F32;
+  const bool s32 = ANY32 && (a.mask & CFA_TF1_STATE_F32), g32 = ANY32 && (a.mask & CFA_TF1_GRAD_F32);
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec2;
        i += (long long)gridDim.x * kBlock) {
     d2 Wv = __builtin_nontemporal_load(reinterpret_cast<const d2*>(a.W) + i);
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void mewma_tf1_f64_vec_kernel(MewmaF64Args 
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       double W = Wv[c];
-      bool w32 = a.mask & CFA_TF1_W_F32;
+      bool w32 = ANY32 && (a.mask & CFA_TF1_W_F32);
       const double lr = 2 * i + c < a.split ? a.lr1 : a.lr2;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
@@ -334,7 +336,11 @@ __global__ __launch_bounds__(kBlock) void mewma_tf1_f64_vec_kernel(MewmaF64Args 
 template <int... Ns>
 static void launch_mewma_f64_vec(int m, unsigned grid, hipStream_t st, const MewmaF64Args& a, long long nvec2,
                                  std::integer_sequence<int, Ns...>) {
-  ((m == Ns + 1 ? (void)(mewma_tf1_f64_vec_kernel<Ns + 1><<<grid, kBlock, 0, st>>>(a, nvec2)) : (void)0), ...);
+  if (a.mask)
+    ((m == Ns + 1 ? (void)(mewma_tf1_f64_vec_kernel<Ns + 1, true><<<grid, kBlock, 0, st>>>(a, nvec2)) : (void)0), ...);
+  else
+    ((m == Ns + 1 ? (void)(mewma_tf1_f64_vec_kernel<Ns + 1, false><<<grid, kBlock, 0, st>>>(a, nvec2)) : (void)0),
+     ...);
 }
 
 template <bool FROM64, int OUT>
