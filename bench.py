@@ -586,6 +586,7 @@ def main():
                                   "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
                                   "autotune": autotune}) if route else None,
                 "placement": info.get("placement"),
+                "halo_carved": info.get("halo_carved"),
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",

@@ -79,16 +79,17 @@ class LoopbackHub:
         self._coll_posts: dict = {}
         self._coll_done: dict = {}
         self.failed: Optional[str] = None
+        self.failed_rank: Optional[int] = None  # the rank whose failure came first (the cause)
         self.groups = [0] * self.world  # exchange calls per rank
         self.messages = [0] * self.world  # non-empty messages received per rank
 
     def transport(self, rank: int) -> "LoopbackTransport":
         return LoopbackTransport(self, rank)
 
-    def fail(self, why: str) -> None:
+    def fail(self, why: str, rank: Optional[int] = None) -> None:
         with self.cv:
             if self.failed is None:
-                self.failed = why
+                self.failed, self.failed_rank = why, rank
             self.cv.notify_all()
 
     def _wait(self, pred: Callable[[], bool], what: str) -> None:
@@ -140,7 +141,7 @@ class LoopbackTransport:
         try:
             self._group(sends, recvs, s)
         except BaseException as exc:
-            hub.fail(f"rank {me}: {exc}")
+            hub.fail(f"rank {me}: {exc}", me)
             raise
 
     def _group(self, sends, recvs, s) -> None:
@@ -233,7 +234,7 @@ class LoopbackTransport:
                 with torch.cuda.stream(s) if s is not None else contextlib.nullcontext():
                     buf.copy_(acc)
         except BaseException as exc:
-            self.hub.fail(f"rank {self.rank}: {exc}")
+            self.hub.fail(f"rank {self.rank}: {exc}", self.rank)
             raise
 
     def allreduce_sum(self, buf: torch.Tensor, stream=None) -> None:
@@ -249,7 +250,7 @@ class LoopbackTransport:
 def run_ranks(world: int, fn: Callable[[int, LoopbackTransport], object], timeout: float = 300.0,
               hub: Optional[LoopbackHub] = None) -> list:
     """Run ``fn(rank, transport)`` for every rank, one host thread each, on a shared hub; returns
-    the results in rank order and re-raises the first rank's exception."""
+    the results in rank order, or re-raises the exception of the rank that failed first."""
     hub = hub or LoopbackHub(world)
     results: list = [None] * world
     errors: list = [None] * world
@@ -262,7 +263,7 @@ def run_ranks(world: int, fn: Callable[[int, LoopbackTransport], object], timeou
             results[r] = fn(r, hub.transport(r))
         except BaseException as exc:  # noqa: BLE001 - re-raised on the caller's thread
             errors[r] = exc
-            hub.fail(f"rank {r}: {type(exc).__name__}: {exc}")
+            hub.fail(f"rank {r}: {type(exc).__name__}: {exc}", r)
 
     threads = [threading.Thread(target=body, args=(r,), name=f"loopback-rank{r}", daemon=True) for r in range(world)]
     for t in threads:
@@ -271,6 +272,9 @@ def run_ranks(world: int, fn: Callable[[int, LoopbackTransport], object], timeou
         t.join(timeout)
         if t.is_alive():
             raise LoopbackError(f"loopback: {t.name} still running after {timeout:.0f} s")
+    first = hub.failed_rank
+    if first is not None and errors[first] is not None:
+        raise errors[first]  # the cause, not another rank's "gave up waiting"
     for e in errors:
         if e is not None:
             raise e

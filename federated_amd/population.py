@@ -372,7 +372,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                                 stacks=stacks)
     info = {"partition": partition, "device_groups": gd, "param_slices": gp,
             "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L,
-            "placement": placement}
+            "placement": placement, "halo_carved": shard.carved}
     if route is not None:
         info["route"] = route.summary()
         info["route_digest"] = route.digest()

@@ -70,23 +70,27 @@ def test_c4_sharded_4_ranks_loopback(gpu, topology):
             assert np.array_equal(block[i], ref[first + i]), (topology, first + i)
 
 
-def _ring_sharded(gpu, world, D, hl, hr, P, rounds, base, relay=True, staged=True):
+def _ring_sharded(gpu, world, D, hl, hr, P, rounds, base, relay=True, staged=True, partition="devices",
+                  dev_groups=None, slices=False):
     from federated_amd.loopback import LoopbackHub, run_ranks
     from federated_amd.population import make_ring_shard
     full = _seed_full(D, P, base)
 
     def rank_fn(rank, transport):
         shard, info = make_ring_shard(rank, world, D, hl, hr, P, torch.device("cuda"), transport, gpu,
-                                      relay=relay, staged=staged)
+                                      partition=partition, dev_groups=dev_groups, relay=relay, staged=staged)
+        lo, hi = info["slice"]
         cs, ms = torch.cuda.Stream(), torch.cuda.Stream()
         with torch.cuda.stream(cs):
             for i in range(shard.plan.L):
-                shard.models[i].copy_(torch.from_numpy(full[shard.plan.first + i]))
+                shard.models[i].copy_(torch.from_numpy(full[shard.plan.first + i][lo:hi]))
             for _ in range(rounds):
                 shard.round(cs, ms)
                 shard.models.copy_(shard.mixed)
         cs.synchronize()
-        return shard.plan.first, shard.models.cpu().numpy(), info["route"], shard.alphas
+        if slices:
+            return shard.plan.first, shard.models.cpu().numpy(), info.get("route"), shard.alphas, (lo, hi)
+        return shard.plan.first, shard.models.cpu().numpy(), info.get("route"), shard.alphas
 
     hub = LoopbackHub(world)
     res = run_ranks(world, rank_fn, hub=hub)
@@ -116,6 +120,26 @@ def test_bench_plan_n8_loopback_reduced_bucket(gpu):
     for first, block, _, _ in res:
         for i in range(block.shape[0]):
             assert np.array_equal(block[i], ref[first + i]), first + i
+
+
+@pytest.mark.parametrize("world,partition,groups", [(4, "hybrid", 2), (8, "hybrid", 4), (4, "params", None)])
+def test_ring_partitions_loopback(gpu, world, partition, groups):
+    """The bench's other partitions (element slices; device blocks x element slices with the
+    routed halo between ranks holding the same slice), every shard's mixes on this GPU, two rounds
+    fed back, each rank's slice of its devices bit-exact with the unsharded oracle."""
+    D, P, rounds, h = 32, 262_147, 2, 4
+    full, res, hub = _ring_sharded(gpu, world, D, h, h, P, rounds, 8800, partition=partition, dev_groups=groups,
+                                   slices=True)
+    lists = [[(d + o) % D for o in list(range(-h, 0)) + list(range(1, h + 1))] for d in range(D)]
+    ref = _oracle_trajectory(full, lists, lambda d: [1.0 / (2 * h + 1)] * (2 * h), rounds)
+    covered = np.zeros((D, P), dtype=bool)
+    for first, block, _, _, (lo, hi) in res:
+        for i in range(block.shape[0]):
+            assert np.array_equal(block[i], ref[first + i][lo:hi]), (partition, first + i, lo)
+            covered[first + i, lo:hi] = True
+    assert covered.all()  # the ranks' blocks and slices tile the whole population
+    if partition == "hybrid":
+        assert sum(hub.messages) > 0
 
 
 def test_sharded_fedavg_4_ranks_loopback(gpu):

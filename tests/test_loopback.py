@@ -190,3 +190,14 @@ def test_sharded_fedavg_loopback_cpu():
         assert torch.equal(b, out[0])
         d = np.abs(b.numpy().astype(np.float64) - ref).max()
         assert d <= 1e-5 * np.abs(ref).max()
+
+
+def test_the_first_failure_is_the_one_raised():
+    """Rank 2 fails; ranks 0 and 1 then give up waiting. run_ranks raises rank 2's error."""
+    def rank_fn(rank, t):
+        if rank == 2:
+            raise ValueError("the cause")
+        t.exchange([], [(torch.empty(3), 2)])
+
+    with pytest.raises(ValueError, match="the cause"):
+        run_ranks(3, rank_fn, hub=LoopbackHub(3, timeout=30))

@@ -30,7 +30,6 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PEAK = 8000.0
 P_DEFAULT = 25_000_000
 
 # name -> (entry point, algorithmic bytes per launch as a function of P, elements per launch)
