@@ -9,13 +9,16 @@ a wrap-around ring window of K = 8 neighbours. One step = one consensus round of
 population.
 
 Scaling (SURVEY §8 e: "Strong scaling, fixed population"): the population stays D = 128 for
-every N; each of the N ranks (one per GPU) owns D/N devices (``--partition devices``, the
-default): a round is the routed halo exchange of the 2x4 boundary buckets of each rank
-(federated_amd/halo.py: direct plus relayed xGMI paths, sent row by row) overlapped with the
-interior mixes, each boundary device mixing as soon as the rows it reads have landed.
-``--partition params`` splits every bucket's elements over the ranks instead (no exchange);
-``--partition hybrid --device-groups G`` combines the two. ``--devices-per-gpu L`` keeps the
-per-GPU population fixed instead (weak scaling, D = L*N).
+every N. At N > 1 the headline ``value`` uses the element split SURVEY §8 e (1) names for the
+8 x 25M bucket scaling run (``--partition params``: every rank holds a 1/N slice of every
+device's bucket; elements are independent, so there is no exchange). Beside it, in
+``partitions``, the same population, steps and clock on the other partitions: ``devices``
+(contiguous device blocks, north_star's "devices sharded": a round is the routed halo exchange of
+the 2x4 boundary buckets of each rank -- federated_amd/halo.py: direct plus relayed xGMI paths,
+sent row by row -- overlapped with the interior mixes, each boundary device mixing as soon as the
+rows it reads have landed), ``hybrid2`` (from N = 4: 2 device blocks x N/2 slices) and ``weak``
+(128 devices per GPU, D = 128 N). ``--partition devices|hybrid`` makes either the headline;
+``--devices-per-gpu L`` keeps the per-GPU population fixed instead (weak scaling, D = L*N).
 
 Each rank's population stacks are placement-calibrated before the timed region
 (``--placement-candidates``, federated_amd/placement.py: the fastest of 4 allocations per stack,
@@ -58,16 +61,16 @@ def parse():
                    help="simulated devices in the whole population (fixed for every N: strong scaling)")
     p.add_argument("--devices-per-gpu", type=int, default=None,
                    help="weak scaling instead: this many devices per GPU (population = N x this)")
-    p.add_argument("--partition", default="devices", choices=["devices", "params", "hybrid"],
-                   help="devices: contiguous device blocks + halo exchange (default); params: every "
-                        "rank holds a 1/N element slice of every bucket (no exchange); hybrid: "
-                        "--device-groups blocks, each split over N/groups slices")
+    p.add_argument("--partition", default=None, choices=["devices", "params", "hybrid"],
+                   help="params (default at N > 1, SURVEY §8 e (1)): every rank holds a 1/N element slice "
+                        "of every bucket (no exchange); devices: contiguous device blocks + routed halo "
+                        "exchange; hybrid: --device-groups blocks, each split over N/groups slices")
     p.add_argument("--device-groups", type=int, default=None)
     p.add_argument("--no-relay", action="store_true", help="halo on the direct links only")
     p.add_argument("--no-stages", action="store_true",
                    help="whole halo in one exchange step (boundary devices wait for all of it)")
-    p.add_argument("--no-params-leg", action="store_true",
-                   help="N > 1: skip the second, --partition params measurement")
+    p.add_argument("--no-extra-legs", "--no-params-leg", dest="no_extra_legs", action="store_true",
+                   help="N > 1: skip the other partitions' measurements (devices, hybrid2) beside the headline")
     p.add_argument("--no-autotune", action="store_true",
                    help="N > 1: time the relayed route as planned, without first comparing it with "
                         "the direct-only route")
@@ -440,6 +443,11 @@ def main():
         sys.exit("--neighbours must be even (ring window K/2 per side)")
     weak = args.devices_per_gpu is not None
     D = args.devices_per_gpu * world if weak else args.devices
+    if args.partition is None:
+        # SURVEY §8 e (1): "within one bucket elements are independent => split P across G GPUs with
+        # no exchange. Used for the '8 x 25M bucket' scaling run"; the device-sharded population
+        # (with its halo exchange) is measured beside it (partitions.devices)
+        args.partition = "params" if world > 1 and not weak else "devices"
     eng = get_engine(device)
 
     transport, comparable = None, True
@@ -477,27 +485,32 @@ def main():
         if args.placement_release:
             torch.cuda.empty_cache()
 
-    shard, info = build(args.partition)
-    autotune = None
-    if world > 1 and info.get("route", {}).get("relay") and not args.no_autotune:
-        # route autotune, before the timed region: the relayed plan against the direct-only plan,
-        # a few rounds each after warm-up, max over ranks; the faster one is the one timed (the
-        # cost model assumes every link runs at the same rate; this checks it on the node)
+    def build_tuned(partition, devices=None):
+        """The shard of ``partition``; with a relayed route at N > 1, route autotune before any timed
+        region: the relayed plan against the direct-only plan, a few rounds each after warm-up, max
+        over ranks; the faster one is kept (the cost model assumes every link runs at the same
+        rate; this checks it on the node). Returns (shard, info, autotune or None)."""
+        xshard, xinfo = build(partition, devices)
+        if not (world > 1 and xinfo.get("route", {}).get("relay") and not args.no_autotune):
+            return xshard, xinfo, None
         tune_steps = 3
-        watchdog.enter("route autotune")
-        t_rel, _, _ = run_leg(args, shard, world, tune_steps, args.warmup, timed_kernel=False)
-        dshard, dinfo = build(args.partition, relay=False)
+        watchdog.enter(f"route autotune ({partition})")
+        t_rel, _, _ = run_leg(args, xshard, world, tune_steps, args.warmup, timed_kernel=False)
+        dshard, dinfo = build(partition, devices, relay=False)
         t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
-        autotune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
-                    "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
-        if t_dir < t_rel:  # same decision on every rank: both times are maxima over ranks
-            shard, info = dshard, dinfo
-            autotune["chosen"] = "direct"
-        else:
-            del dshard
-            autotune["chosen"] = "relayed"
-        # the losing plan's stacks stay in torch's cache: memory returned to the driver is scrubbed
-        # in the background, which would slow the timed rounds (federated_amd/placement.py)
+        tune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
+                "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
+        # same decision on every rank: both times are maxima over ranks. The losing plan's stacks
+        # stay in torch's cache: memory returned to the driver is scrubbed in the background, which
+        # would slow the timed rounds (federated_amd/placement.py)
+        if t_dir < t_rel:
+            tune["chosen"] = "direct"
+            return dshard, dinfo, tune
+        del dshard
+        tune["chosen"] = "relayed"
+        return xshard, xinfo, tune
+
+    shard, info, autotune = build_tuned(args.partition)
     watchdog.enter("timed rounds")
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
@@ -510,33 +523,42 @@ def main():
     route = info.get("route")
 
     legs = {}
-    if world > 1 and args.partition == "devices" and not args.no_params_leg:
+    if world > 1 and not args.no_extra_legs and not weak:
         del shard
         drop_cached()
-        extra = [("params", None, "same population and steps, every rank holds a 1/N element slice of "
-                                  "every bucket (SURVEY §8 e (1)); no exchange")]
-        if world >= 4 and D % 2 == 0:
-            extra.append(("hybrid", 2, "same population and steps, 2 device blocks, each split over N/2 "
-                                       "element slices; routed halo between ranks holding the same slice"))
-        for part, groups, note in extra:
+        notes = {
+            "params": "same population and steps, every rank holds a 1/N element slice of every bucket "
+                      "(SURVEY §8 e (1)); no exchange",
+            "devices": "same population and steps in contiguous device blocks (north_star: devices sharded); "
+                       "the routed halo of the ring window exchanged every round",
+            "hybrid": "same population and steps, 2 device blocks, each split over N/2 element slices; routed "
+                      "halo between ranks holding the same slice",
+        }
+        extra = [(part, None) for part in ("params", "devices") if part != args.partition]
+        if world >= 4 and D % 2 == 0 and args.partition != "hybrid":
+            extra.append(("hybrid", 2))
+        for part, groups in extra:
             saved, args.device_groups = args.device_groups, groups
             watchdog.enter(f"{part} leg")
-            xshard, xinfo = build(part)
+            xshard, xinfo, xtune = build_tuned(part)
             args.device_groups = saved
             xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
             leg = {"value": round(bytes_total / xel / 1e9, 2), "ms_per_step": round(xel / args.steps * 1e3, 4),
-                   "note": note}
+                   "note": notes[part]}
             if xinfo.get("route"):
                 leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
+                leg["halo_carved"] = xinfo.get("halo_carved")
+            if xtune:
+                leg["autotune"] = xtune
             legs[part if groups is None else f"{part}{groups}"] = leg
             del xshard
             drop_cached()
-        if not args.no_weak_leg and not weak:
-            # weak form for reference: the single-GPU population on every rank (D = 128 N), the
-            # same routed halo now hidden under 120 interior mixes per rank
+        if not args.no_weak_leg:
+            # weak form for reference: the single-GPU population on every rank (D = 128 N) in device
+            # blocks, the routed halo hidden under 120 interior mixes per rank
             Dw = args.devices * world
             watchdog.enter("weak leg")
-            wshard, winfo = build("devices", Dw)
+            wshard, winfo, _ = build_tuned("devices", Dw)
             wel, _, _ = run_leg(args, wshard, world, args.steps, args.warmup, timed_kernel=False)
             legs["weak"] = {"value": round(Dw * (K + 2) * P * 4 * args.steps / wel / 1e9, 2),
                             "ms_per_step": round(wel / args.steps * 1e3, 4), "devices_total": Dw,

@@ -15,7 +15,7 @@ run() {
 }
 run n2_carve python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 \
   bench.py --gpus 2 --transport torch --devices 32 --params 17000000 --placement-candidates 2 --steps 3 --warmup 1 \
-  --no-params-leg --no-weak-leg
+  --partition devices --no-extra-legs --no-weak-leg
 run n8_relay python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29632 \
   bench.py --gpus 8 --transport torch --params 1000000 --steps 3 --warmup 1
 echo "== done"
