@@ -14,7 +14,9 @@ import torch  # noqa: E402
 from federated_amd import _lib  # noqa: E402
 from federated_amd.engine import get_engine  # noqa: E402
 
-P, L, R, STACKS = 25_001_984, 32, 4, 3
+P = int(os.environ.get("MULTI_P", 25_001_984))  # MULTI_P=3125000 MULTI_L=128: one N = 8 params rank
+L = int(os.environ.get("MULTI_L", 32))
+R, STACKS = 4, 3
 eng = get_engine(0)
 lib = _lib.load_experiments()
 fn = lib.cfa_experimental_mix8_multi
