@@ -356,15 +356,17 @@ def test_hostmixer_native_pipeline_concurrent_threads(gpu):
         try:
             torch.cuda.set_device(gpu.device)
             l, nb, al = jobs[i]
-            for _ in range(5):
-                got[i] = mx._mix_native(R._layout_of(l), l, nb, al, None, chunk_elems=50_000, threads=8)
+            for r in range(8):  # helper counts vary between calls and callers (the round-2 deadlock's trigger)
+                got[i] = mx._mix_native(R._layout_of(l), l, nb, al, None, chunk_elems=50_000 if r % 2 else 7_777,
+                                        threads=(8, 2, 5, 16)[(i + r) % 4])
         except Exception as e:  # pragma: no cover - reported below
             errors.append(e)
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    ths = [threading.Thread(target=work, args=(i,), daemon=True) for i in range(len(jobs))]
     for th in ths:
         th.start()
     for th in ths:
         th.join(timeout=60)
+    assert not any(th.is_alive() for th in ths), "a caller did not finish (copy pool stuck?)"
     assert not errors, errors
     for g, w in zip(got, want):
         assert all(np.array_equal(a, b) for a, b in zip(g, w))
