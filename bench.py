@@ -30,8 +30,12 @@ write). Inputs are resident in HBM when the timed region starts.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU; RANK/LOCAL_RANK/WORLD_SIZE from the environment).
-If the RCCL transport cannot be opened the run exits non-zero (``--allow-fallback`` runs on a
-torch.distributed transport instead and marks the line non-comparable).
+The transport (RCCL) is opened after the params headline, which exchanges nothing. If it cannot be
+opened, every leg that exchanges reports the error in ``partitions`` (``--allow-fallback`` runs
+them on a torch.distributed transport instead, marked non-comparable); with a headline that
+exchanges (``--partition devices|hybrid``, weak scaling) the run exits 3. A leg that does not finish
+within ``--leg-seconds`` is reported as an error and the line is printed with the legs measured so
+far.
 """
 from __future__ import annotations
 
@@ -107,6 +111,10 @@ def parse():
     p.add_argument("--watchdog-seconds", type=float, default=900.0,
                    help="end the run with status 124 and the phase it was in if it has not finished "
                         "after this long (a collective that never completes; 0 = off)")
+    p.add_argument("--leg-seconds", type=float, default=240.0,
+                   help="N > 1: budget of each extra leg (partitions beside the headline); a leg that "
+                        "has not finished by then is reported as an error in the line, which is then "
+                        "printed with the legs measured so far (0 = no per-leg budget)")
     return p.parse_args()
 
 
@@ -120,17 +128,37 @@ class Watchdog:
         import threading
         self.phase, self.rank, self._done = "start-up", rank, threading.Event()
         self.t0 = time.perf_counter()
-        if seconds > 0:
-            threading.Thread(target=self._watch, args=(seconds,), daemon=True).start()
+        self._leg = None  # (deadline, budget, on_expire) of a phase entered with its own budget
+        self.seconds = seconds
+        threading.Thread(target=self._watch, daemon=True).start()
 
-    def _watch(self, seconds):
-        if not self._done.wait(seconds):
-            print(f"[bench rank {self.rank}] FATAL: watchdog: not finished after {seconds:.0f} s, "
-                  f"stuck in phase '{self.phase}'", file=sys.stderr, flush=True)
-            os._exit(124)
+    def _watch(self):
+        while not self._done.wait(0.25):
+            now = time.perf_counter()
+            leg = self._leg
+            if leg is not None and now > leg[0]:
+                print(f"[bench rank {self.rank}] watchdog: phase '{self.phase}' did not finish within its "
+                      f"{leg[1]:.0f} s budget", file=sys.stderr, flush=True)
+                os._exit(leg[2](self.phase))
+            if self.seconds > 0 and now - self.t0 > self.seconds:
+                print(f"[bench rank {self.rank}] FATAL: watchdog: not finished after {self.seconds:.0f} s, "
+                      f"stuck in phase '{self.phase}'", file=sys.stderr, flush=True)
+                os._exit(124)
 
     def enter(self, phase: str) -> None:
         self.phase = phase
+
+    def leg(self, phase: str, budget: float, on_expire) -> None:
+        """Enter ``phase`` with a budget of its own (seconds, 0 = none) that holds until ``end_leg``
+        whatever phases are entered meanwhile: if it runs out, ``on_expire(phase)`` runs on the
+        watchdog thread and its return value is the exit status (the N > 1 bench's extra legs: the
+        headline is already measured, so a leg stuck in a collective is reported in the line instead
+        of losing the whole run)."""
+        self.phase = phase
+        self._leg = (time.perf_counter() + budget, budget, on_expire) if budget > 0 else None
+
+    def end_leg(self) -> None:
+        self._leg = None
 
     def done(self) -> None:
         self._done.set()
@@ -287,6 +315,17 @@ def live_traffic(P: int, K: int, timeout: float = 150.0):
 
 class TransportError(RuntimeError):
     pass
+
+
+def agree_all(ok: bool) -> bool:
+    """True when ``ok`` holds on every rank (MIN over the gloo control group; local at N = 1)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(ok)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return int(flag.item()) == 1
 
 
 def open_transport(kind, rank, world, device, allow_fallback=False):
@@ -450,17 +489,32 @@ def main():
         args.partition = "params" if world > 1 and not weak else "devices"
     eng = get_engine(device)
 
-    transport, comparable = None, True
-    if world > 1:
+    # The transport (RCCL) carries the halo of the device-sharded partitions only. The params
+    # headline (every rank a 1/N element slice, no exchange) needs none, so at N > 1 it is measured
+    # first and the transport is opened after it, for the legs that exchange. A transport that cannot
+    # be opened then fails those legs (an "error" entry in the line, never a silent fallback); with
+    # a headline that needs it (--partition devices|hybrid, or weak scaling) the run exits 3.
+    tstate = {"transport": None, "comparable": True, "error": None}
+
+    def ensure_transport():
+        if world == 1 or tstate["transport"] is not None or tstate["error"] is not None:
+            return tstate["transport"]
         watchdog.enter("open transport")
         try:
-            transport, comparable = open_transport(args.transport, rank, world, device, args.allow_fallback)
+            tstate["transport"], tstate["comparable"] = open_transport(args.transport, rank, world, device,
+                                                                       args.allow_fallback)
         except TransportError as exc:
-            print(f"[bench rank {rank}] FATAL: {exc}", file=sys.stderr, flush=True)
-            dist.destroy_process_group()
-            sys.exit(3)
+            tstate["error"] = str(exc)
+        return tstate["transport"]
+
+    headline_exchanges = world > 1 and (args.partition != "params" or weak)
+    if headline_exchanges and ensure_transport() is None:
+        print(f"[bench rank {rank}] FATAL: {tstate['error']}", file=sys.stderr, flush=True)
+        dist.destroy_process_group()
+        sys.exit(3)
 
     def build(partition, devices=None, relay=None):
+        transport = tstate["transport"]
         shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
                                       transport,
                                       eng, partition=partition, dev_groups=args.device_groups,
@@ -472,8 +526,7 @@ def main():
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
             if len(set(digests)) != 1:
-                print(f"[bench rank {rank}] FATAL: route plans differ across ranks", file=sys.stderr, flush=True)
-                sys.exit(4)
+                raise RuntimeError("route plans differ across ranks")
         seed_shard(shard, info, P)
         return shard, info
 
@@ -522,50 +575,6 @@ def main():
     launches_timed = launches_per_step * args.steps
     route = info.get("route")
 
-    legs = {}
-    if world > 1 and not args.no_extra_legs and not weak:
-        del shard
-        drop_cached()
-        notes = {
-            "params": "same population and steps, every rank holds a 1/N element slice of every bucket "
-                      "(SURVEY §8 e (1)); no exchange",
-            "devices": "same population and steps in contiguous device blocks (north_star: devices sharded); "
-                       "the routed halo of the ring window exchanged every round",
-            "hybrid": "same population and steps, 2 device blocks, each split over N/2 element slices; routed "
-                      "halo between ranks holding the same slice",
-        }
-        extra = [(part, None) for part in ("params", "devices") if part != args.partition]
-        if world >= 4 and D % 2 == 0 and args.partition != "hybrid":
-            extra.append(("hybrid", 2))
-        for part, groups in extra:
-            saved, args.device_groups = args.device_groups, groups
-            watchdog.enter(f"{part} leg")
-            xshard, xinfo, xtune = build_tuned(part)
-            args.device_groups = saved
-            xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
-            leg = {"value": round(bytes_total / xel / 1e9, 2), "ms_per_step": round(xel / args.steps * 1e3, 4),
-                   "note": notes[part]}
-            if xinfo.get("route"):
-                leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
-                leg["halo_carved"] = xinfo.get("halo_carved")
-            if xtune:
-                leg["autotune"] = xtune
-            legs[part if groups is None else f"{part}{groups}"] = leg
-            del xshard
-            drop_cached()
-        if not args.no_weak_leg:
-            # weak form for reference: the single-GPU population on every rank (D = 128 N) in device
-            # blocks, the routed halo hidden under 120 interior mixes per rank
-            Dw = args.devices * world
-            watchdog.enter("weak leg")
-            wshard, winfo, _ = build_tuned("devices", Dw)
-            wel, _, _ = run_leg(args, wshard, world, args.steps, args.warmup, timed_kernel=False)
-            legs["weak"] = {"value": round(Dw * (K + 2) * P * 4 * args.steps / wel / 1e9, 2),
-                            "ms_per_step": round(wel / args.steps * 1e3, 4), "devices_total": Dw,
-                            "note": f"{args.devices} devices per GPU (population grown with N), devices partition"}
-            del wshard
-            drop_cached()
-
     result = None
     if rank == 0:
         if weak:
@@ -600,8 +609,8 @@ def main():
                 "param_slices": info["param_slices"],
                 "bytes_per_device_mix": (K + 2) * P * 4,
                 "window_batch": args.window_batch,
-                "transport": transport.name if transport else "none",
-                "comparable": comparable,
+                "transport": tstate["transport"].name if headline_exchanges else "none (no exchange)",
+                "comparable": tstate["comparable"] if headline_exchanges else True,
                 "halo_route": ({k: route[k] for k in ("relay", "stages", "groups", "messages",
                                                      "max_messages_per_rank_group")}
                                | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
@@ -641,8 +650,98 @@ def main():
             rl["achieved_plain_alloc"] = round(plain, 1)
             rl["frac_plain_alloc"] = round(plain / HBM_PEAK_GBS, 4)
             rl["placement_rejected_cached_GiB"] = pl.get("rejected_cached_GiB")
-        if legs:
-            result["partitions"] = legs
+    legs = {}
+    if rank == 0 and world > 1 and not args.no_extra_legs and not weak:
+        result["partitions"] = legs  # filled as the legs finish (a leg over budget reports what it has)
+    if world > 1 and not args.no_extra_legs and not weak:
+        del shard
+        drop_cached()
+        notes = {
+            "params": "same population and steps, every rank holds a 1/N element slice of every bucket "
+                      "(SURVEY §8 e (1)); no exchange",
+            "devices": "same population and steps in contiguous device blocks (north_star: devices sharded); "
+                       "the routed halo of the ring window exchanged every round",
+            "hybrid": "same population and steps, 2 device blocks, each split over N/2 element slices; routed "
+                      "halo between ranks holding the same slice",
+            "weak": f"{args.devices} devices per GPU (population grown with N), devices partition",
+        }
+        extra = [(part, None) for part in ("params", "devices") if part != args.partition]
+        if world >= 4 and D % 2 == 0 and args.partition != "hybrid":
+            extra.append(("hybrid", 2))
+        if not args.no_weak_leg:
+            # weak form for reference: the single-GPU population on every rank (D = 128 N) in device
+            # blocks, the routed halo hidden under 120 interior mixes per rank
+            extra.append(("weak", None))
+
+        import threading
+        report_lock = threading.Lock()
+
+        def report_early(name, why):
+            """Rank 0: print the line once, with the legs measured so far and ``name`` marked with
+            ``why`` (the headline is complete). Returns the exit status, 0."""
+            with report_lock:
+                if rank == 0 and not report_early.done:
+                    out = json.loads(json.dumps(result))
+                    out["partitions"][name] = {"error": why, "note": notes[name.rstrip("0123456789")]}
+                    print(json.dumps(out), flush=True)
+                    report_early.done = True
+            return 0
+        report_early.done = False
+
+        def leg_expired(name):
+            # runs on the watchdog thread of a rank whose leg budget ran out (every rank's budget
+            # starts at the same collective, so they expire together)
+            return lambda phase: report_early(name, f"did not finish within {args.leg_seconds:.0f} s (phase '{phase}')")
+
+        for part, groups in extra:
+            name = part if groups is None else f"{part}{groups}"
+            watchdog.leg(f"{name} leg", args.leg_seconds, leg_expired(name))
+            leg, err = {"note": notes[part]}, None
+            xshard = None
+            try:
+                if part != "params" and ensure_transport() is None:
+                    raise TransportError(tstate["error"])
+                watchdog.enter(f"{name} leg")
+                saved, args.device_groups = args.device_groups, groups
+                try:
+                    if part == "weak":
+                        Dw = args.devices * world
+                        xshard, xinfo, xtune = build_tuned("devices", Dw)
+                        leg_bytes = Dw * (K + 2) * P * 4 * args.steps
+                        leg["devices_total"] = Dw
+                    else:
+                        xshard, xinfo, xtune = build_tuned(part)
+                        leg_bytes = bytes_total
+                finally:
+                    args.device_groups = saved
+                xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
+                leg.update({"value": round(leg_bytes / xel / 1e9, 2), "ms_per_step": round(xel / args.steps * 1e3, 4)})
+                if xinfo.get("route"):
+                    leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
+                    leg["halo_carved"] = xinfo.get("halo_carved")
+                if xtune:
+                    leg["autotune"] = xtune
+                if part != "params":
+                    leg["transport"] = tstate["transport"].name
+                    leg["comparable"] = tstate["comparable"]
+            except Exception as exc:  # reported in the line; every rank takes the same decision below
+                err = f"{type(exc).__name__}: {exc}"
+                print(f"[bench rank {rank}] {name} leg failed: {err}", file=sys.stderr, flush=True)
+            finally:
+                xshard = None
+                drop_cached()
+            try:
+                all_ok = agree_all(err is None)
+            except Exception as exc:  # a peer has left (its leg budget ran out first): report and end
+                print(f"[bench rank {rank}] control plane lost a peer in the {name} leg ({exc})",
+                      file=sys.stderr, flush=True)
+                os._exit(report_early(name, err or f"a rank left during the leg ({type(exc).__name__})"))
+            if not all_ok:
+                leg = {"error": err or "failed on another rank", "note": notes[part]}
+            legs[name] = leg
+            watchdog.end_leg()
+        if rank == 0 and not legs:
+            result.pop("partitions", None)
     if world > 1:
         dist.barrier()
     # CPU baselines: rank 0, N = 1 only (bounded samples).
@@ -666,8 +765,8 @@ def main():
             from federated_amd.staging import measure_e2e
             result["e2e"] = measure_e2e(eng, P, K)
         print(json.dumps(result), flush=True)
-    if transport is not None:
-        transport.close()
+    if tstate["transport"] is not None:
+        tstate["transport"].close()
     if world > 1:
         dist.destroy_process_group()
     watchdog.done()

@@ -144,7 +144,7 @@ class CopyPool {
     for (long spin = 0;; ++spin) {
       const uint64_t s = state_.load(std::memory_order_acquire);
       if ((s >> 8) != seen) return s;
-      if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
+      if ((spin & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
         std::unique_lock<std::mutex> g(mu_);
         uint64_t w = 0;
         cv_.wait(g, [&] {
@@ -153,7 +153,8 @@ class CopyPool {
         });
         return w;
       }
-      cpu_relax();
+      if (spin < 256) cpu_relax();
+      else std::this_thread::yield();  // oversubscribed: give the core to the caller
     }
   }
 

@@ -26,7 +26,7 @@
 
 namespace {
 
-constexpr size_t kArena = size_t(1) << 16;  // bytes per source / destination arena
+constexpr size_t kArena = size_t(1) << 13;  // bytes per source / destination arena
 
 int failures = 0;
 
@@ -49,7 +49,7 @@ void one_run(cfa::CopyPool& pool, Arena& a, std::mt19937_64& rng, long r, int th
   std::vector<std::pair<size_t, size_t>> ranges;
   size_t off = 0;
   for (int j = 0; j < njobs && off < kArena; ++j) {
-    std::uniform_int_distribution<size_t> gap_d(0, 64), len_d(1, 1024);
+    std::uniform_int_distribution<size_t> gap_d(0, 8), len_d(1, 128);
     off += gap_d(rng);
     const size_t len = std::min(len_d(rng), kArena - std::min(off, kArena));
     if (len == 0) break;
@@ -104,11 +104,16 @@ int main(int argc, char** argv) {
                 static_cast<unsigned long long>(pool.generation()));
   }
   {  // phase 3: a zero timeout may break the pool; later runs must still be complete
+    // 16 jobs of 4 MiB on 8 threads: helpers are still inside a copy when the caller, done with its
+    // own share, finds the zero timeout spent. The buffers are declared before the pool, so they
+    // outlive the stragglers the pool's destructor joins.
+    constexpr size_t kBig = size_t(4) << 20;
+    std::vector<unsigned char> big_src(16 * kBig, 1), big_dst(16 * kBig, 0);
+    Arena b;
     cfa::CopyPool pool;
-    Arena a, b;
     std::mt19937_64 rng(seed + 99);
     std::vector<cfa::Copy> jobs;
-    for (size_t o = 0; o < kArena; o += 512) jobs.push_back({a.dst.data() + o, a.src.data() + o, 512});
+    for (size_t o = 0; o < big_src.size(); o += kBig) jobs.push_back({big_dst.data() + o, big_src.data() + o, kBig});
     const bool ok = pool.run(jobs.data(), jobs.size(), 8, std::chrono::nanoseconds(0));
     // wait for stragglers of the timed-out run through the destructor's join below; meanwhile
     // the pool must serve complete runs on other buffers

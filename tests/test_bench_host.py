@@ -71,3 +71,24 @@ def test_watchdog_ends_a_stuck_run_with_its_phase():
     assert "[bench rank 3] FATAL: watchdog" in stuck.stderr and "'timed rounds'" in stuck.stderr
     ok = subprocess.run([sys.executable, "-c", code % (ROOT, 30, 0.1)], capture_output=True, text=True, timeout=60)
     assert ok.returncode == 0 and "finished" in ok.stdout
+
+
+def test_watchdog_leg_budget_reports_and_exits_with_its_status():
+    """An extra N > 1 leg past its own budget runs the leg's on_expire (which prints the line with
+    the legs measured so far) and exits with its status, whatever phases were entered inside the
+    leg; after end_leg the budget no longer applies."""
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "w = bench.Watchdog(60, 0)\n"
+            "def expire(phase):\n"
+            "    print('partial line, stuck in', phase, flush=True); return 0\n"
+            "w.leg('devices leg', %s, expire); w.enter('route autotune (devices)'); time.sleep(%s)\n"
+            "w.end_leg(); w.enter('after'); time.sleep(%s); w.done(); print('finished')")
+    stuck = subprocess.run([sys.executable, "-c", code % (ROOT, 0.5, 30, 0)], capture_output=True, text=True,
+                           timeout=60)
+    assert stuck.returncode == 0
+    assert "partial line, stuck in route autotune (devices)" in stuck.stdout and "finished" not in stuck.stdout
+    assert "did not finish within its 0 s budget" in stuck.stderr or "budget" in stuck.stderr
+    ok = subprocess.run([sys.executable, "-c", code % (ROOT, 0.5, 0.1, 1.0)], capture_output=True, text=True,
+                        timeout=60)
+    assert ok.returncode == 0 and "finished" in ok.stdout and "partial" not in ok.stdout

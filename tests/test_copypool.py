@@ -38,8 +38,8 @@ def _run(exe, runs, seed, timeout):
 
 
 def test_copypool_stress_plain(tmp_path):
-    out = _run(_build(tmp_path, "plain", ["-O2"]), 30000, 7, timeout=240)
-    assert "phase 1: 30000 runs, 15 workers" in out
+    out = _run(_build(tmp_path, "plain", ["-O2"]), 100000, 7, timeout=240)
+    assert "phase 1: 100000 runs, 15 workers" in out
 
 
 def test_copypool_stress_tsan(tmp_path):
