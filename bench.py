@@ -621,6 +621,10 @@ def main():
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
+                "rows_note": (f"each rank's rows are {shard_P(info, P)} elements; below about 6M elements the "
+                              "ring window's 9 rows fit the 256 MB Infinity Cache, so a mix re-reads the 8 rows it "
+                              "shares with the previous device's mix from it (DESIGN.md §5); value counts "
+                              "algorithmic bytes") if world > 1 and info["partition"] == "params" else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -74,6 +74,31 @@ static int auto_vec(int n) { return (n + 1) * 4 <= 40 ? 4 : ((n + 1) * 2 <= 40 ?
 // lane at K = 2/4/8/12 on two boxes): one workgroup per CU (one wave per SIMD) at every fan-in,
 // two float4 per lane except for 3-5 neighbours, where one is best. Sequential rule only.
 static int mix_auto_vec(int n) { return (n >= 3 && n <= 5) ? 1 : ((n + 1) * 2 <= 40 ? 2 : 1); }
+// ... for buckets of 8M elements and more. Shorter mixes need more loads in flight than one
+// wave per SIMD issues (round 3, tools/probe/slice_shape.py on placement-calibrated populations,
+// P = 0.5M-25M; profiles/r03_slice_shape_k{4,8}.jsonl for the sweep, r03_ab_shape.jsonl for two
+// rounds of A/B against the one-workgroup shape at K = 2/4/8/16). Four workgroups per CU:
+//   - with one float4 per lane from 512K to 1.5M elements (1M: +2-13% in 3 of 4 A/B pairs);
+//   - with four float4 from 1.5M to 8M (3.125M, the N = 8 bench rank's slice: +6-13% on ring
+//     windows, +7% on rows no two consecutive mixes share; 6.25M: +1-5%);
+//   - with two for 10-16 neighbours from 1.5M to 3M (+3-5%; neutral to -2% above).
+// Below 512K elements (e.g. the drop-in pipeline's 128K chunks read over PCIe; at 500K the A/B
+// pairs split both ways at K = 4 and 16) the shape is unchanged.
+static void mix_auto_shape(int n, long long nvec, int& blocks_per_cu, int& vec) {
+  const long long elems = nvec * 4;
+  const bool narrow = (n + 1) * 4 <= 40;
+  blocks_per_cu = 4;
+  if (elems >= (1LL << 19) && elems < (3LL << 19)) {
+    vec = 1;
+  } else if (elems >= (3LL << 19) && elems < (8LL << 20) && narrow) {
+    vec = 4;
+  } else if (elems >= (3LL << 19) && elems < (3LL << 20) && !narrow) {
+    vec = 2;
+  } else {
+    blocks_per_cu = 1;
+    vec = mix_auto_vec(n);
+  }
+}
 static cfa_launch_t read_tune() {
   cfa_launch_t t{kAutoBlocks, 0, 1};
   if (const char* s = getenv("CFA_BLOCKS_PER_CU")) {

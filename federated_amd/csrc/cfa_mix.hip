@@ -251,11 +251,13 @@ static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, 
   // (the sequential rule only: the linear closed form measured 0.752 with it against 0.790 with
   // two workgroups x 4 float4 on the same buffers, profiles/r02_s3_kernel_rooflines_vec_same.jsonl)
   const bool own = t.blocks_per_cu == kAutoBlocks && RULE == CFA_RULE_SEQUENTIAL;
+  int own_bpc = 1, own_vec = 1;
+  if (own) mix_auto_shape(n, nvec, own_bpc, own_vec);
   const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane)
-                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : (own ? mix_auto_vec(n) : auto_vec(n)));
+                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : (own ? own_vec : auto_vec(n)));
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   cfa_launch_t shape = t;
-  if (own) shape.blocks_per_cu = 1;
+  if (own) shape.blocks_per_cu = own_bpc;
   const unsigned grid = grid_for(tiles, shape);
   if (U == 4) {
     if (t.nontemporal) launch_vec_u<RULE, 4, true>(n, grid, st, out, f, nvec);

@@ -234,9 +234,11 @@ typedef struct {
   int nontemporal;    /* 1 = nontemporal (streaming) loads/stores for once-touched buckets */
 } cfa_launch_t;
 
-/* cfa_mix_seq_f32 with an explicit launch configuration (NULL = library default: one workgroup
- * per CU and 2 vectors per lane, 1 for 3-5 neighbours, from a sweep on placement-calibrated
- * buckets; an explicit configuration with vec_per_lane = 0 takes round 1's auto width). */
+/* cfa_mix_seq_f32 with an explicit launch configuration (NULL = library default, from sweeps on
+ * placement-calibrated buckets: one workgroup per CU and 2 vectors per lane, 1 for 3-5
+ * neighbours; from 512K to 1.5M elements four workgroups per CU with 1 vector per lane, from 1.5M
+ * to 8M four with 4 (up to 9 neighbours; with 2 below 3M above that); an explicit configuration
+ * with vec_per_lane = 0 takes round 1's auto width). */
 CFA_API int cfa_mix_seq_ex_f32(float* out, const float* local, const float* const* nbrs,
                                const float* alphas, int n, size_t P, const cfa_launch_t* launch,
                                void* stream);
