@@ -7,20 +7,27 @@
 // at MNIST_dataset/consensus/consensus_v3.py:144-157), so the pool is entered concurrently.
 //
 // Protocol (one run at a time; a caller that finds the pool busy copies on its own thread):
-//   - run() owns the job list for the run (copied into pool storage), resets the claim counter
-//     and the completion count, then publishes ONE atomic word  state = gen << 8 | helpers.
-//   - A worker takes its part in a run from a single load of that word: worker `id` helps
-//     generation g exactly when it observes g and id < helpers(g). The generation and the helper
+//   - run() owns the job list for the run (copied into pool storage), resets the claim and the
+//     completion counters, then publishes ONE atomic word  state = gen << 8 | helpers  (open).
+//   - A worker takes its part in a run from a single load of that word: worker `id` may help
+//     generation g when it observes g open and id < helpers(g). The generation and the helper
 //     count can never come from two different runs.
-//   - A helper of generation g is counted in pending(g), so run g cannot return (and run g + 1
-//     cannot start) until that helper has finished with the job list. A worker therefore only
-//     ever skips generations that did not need it, and never touches the job list of a run it
-//     did not claim.
-//   - run()'s wait is bounded: past `timeout` the pool is marked broken, run() returns false so
+//   - Joining is a claim: the worker enters (active += 1), then re-reads the word and drains jobs
+//     only if it still holds exactly the open word it observed; otherwise it leaves (active -= 1)
+//     without touching the job list.
+//   - run() drains jobs itself, waits until every job has completed, then CLOSES the run (state
+//     = gen << 8 | 0) and waits until no worker is active. Both the claim and the close are a
+//     store followed by a load of the other side's word (sequentially consistent), so either the
+//     worker sees the run closed and leaves, or run() sees the worker active and waits for it: no
+//     worker touches a job list after its run returned. Late workers simply miss the run, so run()
+//     never waits for a helper that was not needed (with more helpers than free cores, waiting for
+//     every helper to wake had cost a scheduling round per run).
+//   - run()'s waits are bounded: past `timeout` the pool is marked broken, run() returns false so
 //     the caller can fail with a message instead of spinning forever, and every later run copies
 //     on its caller's thread, so the pool's job list and counters are left to the stragglers.
-// Workers spin for ~50 us after each run before parking on a condition variable, so the runs of
-// one pipelined call (one per chunk, tens of microseconds apart) do not pay a futex wake-up each.
+// Workers spin (pausing, then yielding the core) for ~50 us after each run before parking on a
+// condition variable, so the runs of one pipelined call (one per chunk, tens of microseconds
+// apart) do not pay a futex wake-up each.
 #ifndef CFA_COPYPOOL_H
 #define CFA_COPYPOOL_H
 
@@ -59,8 +66,9 @@ class CopyPool {
   CopyPool(const CopyPool&) = delete;
   CopyPool& operator=(const CopyPool&) = delete;
 
-  // Stops and joins the workers. Only for pools that are not broken (a broken pool may have a
-  // worker stuck in a copy; the library's process-wide pool is never destroyed).
+  // Stops and joins the workers (a broken pool's straggler is joined after its copy finishes, so
+  // the buffers of a timed-out run must outlive the pool; the library's process-wide pool is
+  // never destroyed).
   ~CopyPool() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -73,7 +81,7 @@ class CopyPool {
   }
 
   // Copies every job, on up to `threads` threads (the caller included). Returns false only when
-  // the helpers did not finish within `timeout` (the pool is then broken; see above).
+  // the jobs or the helpers did not finish within `timeout` (the pool is then broken; see above).
   bool run(const Copy* jobs, size_t njobs, int threads,
            std::chrono::nanoseconds timeout = std::chrono::seconds(30)) {
     if (njobs == 0) return true;
@@ -87,28 +95,17 @@ class CopyPool {
     ensure(helpers);
     jobs_.assign(jobs, jobs + njobs);
     next_.store(0, std::memory_order_relaxed);
-    pending_.store(helpers, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> g(mu_);  // under the lock: a parking worker cannot miss it
-      publish(helpers);                    // release: jobs_, next_, pending_ happen-before
+      publish(helpers);                    // release: jobs_, next_, done_ happen-before
     }
     cv_.notify_all();
     drain(jobs_);
     const auto t0 = std::chrono::steady_clock::now();
-    for (long spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
-      if (spin < 4096) {
-        cpu_relax();
-        continue;
-      }
-      std::this_thread::yield();
-      if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > timeout) {
-        // stragglers may still read jobs_ and bump next_ / pending_: a broken pool never touches
-        // them again (every later run copies on its caller's thread)
-        broken_.store(true, std::memory_order_relaxed);
-        return false;
-      }
-    }
-    return true;
+    if (!wait([&] { return done_.load(std::memory_order_acquire) == njobs; }, t0, timeout)) return false;
+    close();
+    return wait([&] { return active_.load(std::memory_order_seq_cst) == 0; }, t0, timeout);
   }
 
   bool broken() const { return broken_.load(std::memory_order_relaxed); }
@@ -119,7 +116,33 @@ class CopyPool {
   // Caller holds mu_. Bumps the generation and sets the helper count in one store.
   void publish(int helpers) {
     const uint64_t gen = (state_.load(std::memory_order_relaxed) >> 8) + 1;
-    state_.store(gen << 8 | uint64_t(helpers), std::memory_order_release);
+    state_.store(gen << 8 | uint64_t(helpers), std::memory_order_seq_cst);
+  }
+
+  // The current run takes no more helpers: same generation, helper count 0 (a worker waiting for
+  // a new generation does not wake for it; a joining worker re-reads the word and leaves).
+  void close() {
+    const uint64_t s = state_.load(std::memory_order_relaxed);
+    state_.store(s & ~uint64_t(0xff), std::memory_order_seq_cst);
+  }
+
+  // Spins (then yields) until pred(); past `timeout` marks the pool broken and returns false:
+  // stragglers may still read jobs_ and bump the counters, and a broken pool never touches them
+  // again (every later run copies on its caller's thread).
+  template <class Pred>
+  bool wait(Pred pred, std::chrono::steady_clock::time_point t0, std::chrono::nanoseconds timeout) {
+    for (long spin = 0; !pred(); ++spin) {
+      if (spin < 4096) {
+        cpu_relax();
+        continue;
+      }
+      std::this_thread::yield();
+      if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > timeout) {
+        broken_.store(true, std::memory_order_relaxed);
+        return false;
+      }
+    }
+    return true;
   }
 
   // Caller holds run_mu_, so the generation cannot move while workers are created.
@@ -134,11 +157,14 @@ class CopyPool {
 
   void drain(const std::vector<Copy>& jobs) {
     for (size_t i = next_.fetch_add(1, std::memory_order_relaxed); i < jobs.size();
-         i = next_.fetch_add(1, std::memory_order_relaxed))
+         i = next_.fetch_add(1, std::memory_order_relaxed)) {
       std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
+      done_.fetch_add(1, std::memory_order_release);
+    }
   }
 
-  // One load of state_ that differs from `seen`'s generation: spin, then park.
+  // One load of state_ whose generation differs from `seen`: spin (pausing, then yielding the
+  // core, so a caller sharing it with idle workers is not held up), then park.
   uint64_t await(uint64_t seen) {
     const auto t0 = std::chrono::steady_clock::now();
     for (long spin = 0;; ++spin) {
@@ -154,7 +180,7 @@ class CopyPool {
         return w;
       }
       if (spin < 256) cpu_relax();
-      else std::this_thread::yield();  // oversubscribed: give the core to the caller
+      else std::this_thread::yield();
     }
   }
 
@@ -163,9 +189,10 @@ class CopyPool {
       const uint64_t s = await(seen);
       seen = s >> 8;
       if (stop_.load(std::memory_order_relaxed)) return;
-      if (id >= int(s & 0xff)) continue;  // not a helper of generation `seen`
-      drain(jobs_);  // stable until pending_ reaches zero
-      pending_.fetch_sub(1, std::memory_order_acq_rel);
+      if (id >= int(s & 0xff)) continue;  // not a helper of generation `seen` (or already closed)
+      active_.fetch_add(1, std::memory_order_seq_cst);
+      if (state_.load(std::memory_order_seq_cst) == s) drain(jobs_);  // still open: jobs_ is stable
+      active_.fetch_sub(1, std::memory_order_release);
     }
   }
 
@@ -173,9 +200,9 @@ class CopyPool {
   std::condition_variable cv_;
   std::vector<std::thread> workers_;
   std::vector<Copy> jobs_;  // the current run's job list (pool-owned: outlives the caller's)
-  std::atomic<size_t> next_{0};
-  std::atomic<int> pending_{0};
-  std::atomic<uint64_t> state_{0};  // gen << 8 | helpers
+  std::atomic<size_t> next_{0}, done_{0};
+  std::atomic<int> active_{0};
+  std::atomic<uint64_t> state_{0};  // gen << 8 | helpers (0 once the run is closed)
   std::atomic<bool> stop_{false}, broken_{false};
 };
 

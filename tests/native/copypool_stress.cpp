@@ -15,6 +15,7 @@
 // thread), and a zero timeout exercises the broken-pool path.
 //
 // usage: copypool_stress RUNS SEED
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,7 +75,12 @@ void one_run(cfa::CopyPool& pool, Arena& a, std::mt19937_64& rng, long r, int th
 
 }  // namespace
 
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int main(int argc, char** argv) {
+  auto t0 = std::chrono::steady_clock::now();
   const long runs = argc > 1 ? std::atol(argv[1]) : 100000;
   const unsigned long long seed = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1;
   static const int helper_cycle[] = {1, 3, 7, 15};
@@ -86,8 +92,9 @@ int main(int argc, char** argv) {
     for (long r = 0; r < runs && failures == 0; ++r) one_run(pool, a, rng, r, helper_cycle[r % 4] + 1);
     if (pool.generation() == 0) fail("pool never published a run", -1);
     if (pool.broken()) fail("pool broken after phase 1", -1);
-    std::printf("phase 1: %ld runs, %d workers, generation %llu\n", runs, pool.workers(),
-                static_cast<unsigned long long>(pool.generation()));
+    std::printf("phase 1: %ld runs, %d workers, generation %llu (%.1f s)\n", runs, pool.workers(),
+                static_cast<unsigned long long>(pool.generation()), seconds_since(t0));
+    t0 = std::chrono::steady_clock::now();
   }
   {  // phase 2: four callers at once on one pool (each run either owns the pool or copies alone)
     cfa::CopyPool pool;
@@ -100,8 +107,8 @@ int main(int argc, char** argv) {
         for (long r = 0; r < per; ++r) one_run(pool, a, rng, r, helper_cycle[(r + c) % 4] + 1);
       });
     for (std::thread& t : callers) t.join();
-    std::printf("phase 2: 4 callers x %ld runs, generation %llu\n", per,
-                static_cast<unsigned long long>(pool.generation()));
+    std::printf("phase 2: 4 callers x %ld runs, generation %llu (%.1f s)\n", per,
+                static_cast<unsigned long long>(pool.generation()), seconds_since(t0));
   }
   {  // phase 3: a zero timeout may break the pool; later runs must still be complete
     // 16 jobs of 4 MiB on 8 threads: helpers are still inside a copy when the caller, done with its
