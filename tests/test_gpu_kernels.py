@@ -38,6 +38,23 @@ def test_mix_seq_bitexact(gpu, n):
         assert np.array_equal(out.cpu().numpy(), ref), (n, P)
 
 
+@pytest.mark.parametrize("n", [2, 4, 8, 12, 16])
+def test_mix_seq_bitexact_across_launch_shape_bands(gpu, n):
+    """The default launch shape depends on the bucket size (cfa_internal.h mix_auto_shape): one
+    workgroup per CU from 8M elements, four below (1 float4 per lane from 512K, 4 from 1.5M, 2 for
+    more than 9 neighbours up to 3M). Sizes on both sides of every band edge, with ragged tails."""
+    rng = np.random.default_rng(300 + n)
+    for P in [524_287, 524_293, 1_572_861, 1_572_873, 2_000_003, 3_145_731, 3_145_741, 8_388_607,
+              8_388_613]:
+        local = _rand(rng, 1, P)[0]
+        nbrs = _rand(rng, n, P)
+        alphas = [1.0 / (n + 1)] * n
+        ref = O.sequential_mix(local, nbrs, alphas)
+        out = torch.empty(P, dtype=torch.float32, device="cuda")
+        gpu.mix_seq(out, _dev(local), [_dev(x) for x in nbrs], alphas)
+        assert np.array_equal(out.cpu().numpy(), ref), (n, P)
+
+
 def test_mix_seq_varied_alphas_and_inplace(gpu):
     rng = np.random.default_rng(7)
     P = 1_000_003
