@@ -165,3 +165,64 @@ def test_sharded_fedavg_4_ranks_loopback(gpu):
     for b in out:
         assert np.array_equal(b, out[0])
         assert np.abs(b.astype(np.float64) - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("partition,groups", [("devices", None), ("hybrid", 2)])
+def test_bench_plan_n8_loopback_full_bucket(gpu, partition, groups):
+    """bench.py's N = 8 plans at the BASELINE bucket size (128 devices x 25M fp32, K = 8 ring
+    window): the relayed, staged device-block plan and the hybrid (2 device blocks x 4 element
+    slices). One sharded round over the loopback equals the unsharded population round on the same
+    GPU row for row (halo rows, relay slots and slices at their full-size offsets), and two
+    boundary devices of the unsharded round equal the CPU oracle."""
+    from federated_amd.loopback import LoopbackHub, run_ranks
+    from federated_amd.population import make_ring_shard
+    D, world, P, h, base = 128, 8, 25_000_000, 4, 9900
+    dev = torch.device("cuda")
+
+    def seed(t, g, lo, hi):
+        gen = torch.Generator(device=dev).manual_seed(base + g)
+        if (lo, hi) == (0, P):
+            t.normal_(generator=gen)
+            return
+        full = torch.empty(P, dtype=torch.float32, device=dev)
+        full.normal_(generator=gen)
+        t.copy_(full[lo:hi])
+
+    ref, _ = make_ring_shard(0, 1, D, h, h, P, dev, None, gpu)
+    for g in range(D):
+        seed(ref.models[g], g, 0, P)
+    ref.round()
+    torch.cuda.synchronize()
+
+    def rank_fn(rank, transport):
+        shard, info = make_ring_shard(rank, world, D, h, h, P, dev, transport, gpu, partition=partition,
+                                      dev_groups=groups)
+        lo, hi = info["slice"]
+        cs, ms = torch.cuda.Stream(), torch.cuda.Stream()
+        with torch.cuda.stream(cs):
+            for i in range(shard.plan.L):
+                seed(shard.models[i], shard.plan.first + i, lo, hi)
+            shard.round(cs, ms)
+        cs.synchronize()
+        bad = [shard.plan.first + i for i in range(shard.plan.L)
+               if not torch.equal(shard.mixed[i], ref.mixed[shard.plan.first + i][lo:hi])]
+        return bad, info.get("route"), (lo, hi), shard.plan.first, shard.plan.L
+
+    hub = LoopbackHub(world)
+    res = run_ranks(world, rank_fn, hub=hub)
+    assert sum(hub.messages) > 0
+    assert all(not bad for bad, *_ in res), [bad for bad, *_ in res]
+    covered = np.zeros(D, dtype=np.int64)
+    for _, _, (lo, hi), first, L in res:
+        covered[first:first + L] += hi - lo
+    assert (covered == P).all()  # blocks and slices tile every bucket exactly once
+    if partition == "devices":
+        assert res[0][1]["relay"] is True
+    alphas = [1.0 / (2 * h + 1)] * (2 * h)
+    for g in (15, 16):  # the last device of rank 0's block and the first of rank 1's
+        rows = [ref.models[(g + o) % D].cpu().numpy() for o in list(range(-h, 0)) + list(range(1, h + 1))]
+        want = sequential_mix(ref.models[g].cpu().numpy(), rows, alphas)
+        assert np.array_equal(ref.mixed[g].cpu().numpy(), want), g
+        del rows, want
+    del ref
+    torch.cuda.empty_cache()
