@@ -99,8 +99,11 @@ def parse():
     p.add_argument("--no-live-traffic", action="store_true",
                    help="N = 1: do not measure roofline.traffic with rocprofv3 PMC passes in this run "
                         "(the committed profiles/ value is reported instead)")
-    p.add_argument("--e2e", action="store_true",
-                   help="also measure the host-resident path (pinned H2D + mix + D2H) on rank 0")
+    p.add_argument("--e2e", dest="e2e", action="store_true", default=True,
+                   help="(default at N = 1) also measure the host-resident path on rank 0: the same mix with "
+                        "the buckets in pinned host memory, serial H2D + mix + D2H, chunk-pipelined, and "
+                        "zero-copy over PCIe (reported under \"e2e\", never as value)")
+    p.add_argument("--no-e2e", dest="e2e", action="store_false")
     p.add_argument("--placement-candidates", type=int, default=4,
                    help="allocate each population stack this many times and keep the fastest, timed "
                         "with the population's own mix before the timed region (federated_amd/placement.py; "
@@ -765,7 +768,7 @@ def main():
                 rl["traffic"] = round(live, 1)
                 rl["traffic_over_algorithmic"] = round(live / rl["bytes_per_launch"], 5)
             rl["traffic_source"] = note if live is not None else f"committed profile ({note})"
-        if args.e2e:
+        if args.e2e and world == 1:
             from federated_amd.staging import measure_e2e
             result["e2e"] = measure_e2e(eng, P, K)
         print(json.dumps(result), flush=True)

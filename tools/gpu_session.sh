@@ -19,7 +19,7 @@ set -u
 TAG=${1:?tag}; shift
 OUT=gpurun_out; mkdir -p "$OUT"; cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic"
+BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic --no-e2e"
 step() {
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
