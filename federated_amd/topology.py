@@ -117,6 +117,16 @@ def window_shape(lists: Sequence[Sequence[int]], alphas: Sequence[Sequence[float
     return None
 
 
+def _zero_on(t: torch.Tensor, stream) -> None:
+    """Zero ``t`` in the order of ``stream`` (the stream the kernel that accumulates into it runs
+    on; None = the current stream), so the reset cannot race a launch on another stream."""
+    if stream is None:
+        t.zero_()
+        return
+    with torch.cuda.stream(stream):
+        t.zero_()
+
+
 class PopulationRound:
     """A population of D device buckets resident in HBM, mixed in ONE launch per round."""
 
@@ -195,7 +205,7 @@ class PopulationRound:
         if self._tf1:
             mode, cb, ce = self._compress
             if mode:
-                self.kept.zero_()
+                _zero_on(self.kept, stream)
             self.engine.population_tf1(dst, src, *self.tables, D, P, stream, mode, cb, ce, self.kept if mode else None)
             return
         self.engine.population(dst, src, *self.tables, D, RULE_SEQUENTIAL, P, stream)
@@ -308,7 +318,7 @@ class Tf1PopulationRound:
         src, dst = self._tables[self._rot]
         mode, cb, ce = self._compress
         if mode:
-            self.kept.zero_()
+            _zero_on(self.kept, stream)
         self.engine.population_tf1(dst, src, *self._csr, self.D, self.P, stream, mode, cb, ce,
                                    self.kept if mode else None)
         self._rot = (self._rot + 2) % 3  # (current, previous, out) <- (out, current, previous)
