@@ -42,6 +42,7 @@ def test_copypool_stress_plain(tmp_path):
     assert "phase 1: 100000 runs, 15 workers" in out
 
 
+@pytest.mark.timeout(900)  # 1-2 minutes on 8 CPUs; headroom over pytest.ini's 300 s on a slower host
 def test_copypool_stress_tsan(tmp_path):
-    out = _run(_build(tmp_path, "tsan", ["-O2", "-g", "-fsanitize=thread"]), 100000, 11, timeout=600)
+    out = _run(_build(tmp_path, "tsan", ["-O2", "-g", "-fsanitize=thread"]), 100000, 11, timeout=840)
     assert "phase 1: 100000 runs, 15 workers" in out

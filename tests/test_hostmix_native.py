@@ -50,5 +50,6 @@ def test_host_pipeline_concurrent_callers_plain(tmp_path):
         _run(exe, 4, 300, seed, timeout=120)
 
 
+@pytest.mark.timeout(600)  # about 30 s on 8 CPUs; headroom over pytest.ini's 300 s on a slower host
 def test_host_pipeline_concurrent_callers_tsan(tmp_path):
-    _run(_build(tmp_path, "tsan", ["-O1", "-g", "-fsanitize=thread"]), 4, 150, 5, timeout=300)
+    _run(_build(tmp_path, "tsan", ["-O1", "-g", "-fsanitize=thread"]), 4, 150, 5, timeout=540)
