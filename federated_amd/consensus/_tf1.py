@@ -104,6 +104,17 @@ def gpu_mix(local4: Sequence, nbr_models: Sequence, alphas: Sequence[float], com
     return mixer().mix_tf1(list(local4), nbr_models, alphas, compress)
 
 
+def no_neighbour_error() -> UnboundLocalError:
+    """The error the TF1 modules raise when a mixing epoch has no neighbour, or when a federated
+    process is told it is the only device: their result variables are assigned only inside the
+    neighbour loop (cfa.py:107-154, the loop :119-130 and its use :141; cfa_ge_2stage.py:189-211
+    and :449-463), so Python raises UnboundLocalError. The drop-ins raise the same error at the
+    same point of the protocol, so a driver configured that way (N = 1 on the k-regular window
+    leaves every interior device without a neighbour, cfa.py:14-32) fails as it does on the
+    reference instead of running on with an unmixed model."""
+    return UnboundLocalError("local variable 'W_up_l1' referenced before assignment")
+
+
 def publish(dev: int, ep: int, W1, b1, W2, b2, **extra) -> None:
     """Write datamat{dev}_{ep}.mat with the four tensors plus any extra keys (epoch,
     loss_sample, counter_param), as the reference's savemat calls do."""

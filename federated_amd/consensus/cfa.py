@@ -60,15 +60,15 @@ class CFA_process:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2
         if self.devices <= 1:
-            return n_W_l1, n_b_l1, n_W_l2, n_b_l2
+            raise _tf1.no_neighbour_error()  # federated with one device: nothing assigns the result (:107, :154)
         if epoch == 0:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2
         models, _, _ = _tf1.load_neighbour_models(self.neighbor_vec, epoch - 1)
         alphas = [eps_t_control * f for f in self._alphas()]
-        if models:
-            (W1, b1, W2, b2), _ = _tf1.gpu_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], models, alphas)
-        else:
-            W1, b1, W2, b2 = n_W_l1, n_b_l1, n_W_l2, n_b_l2
+        if not models:  # the reference publishes (:132-139), then reads the unassigned result (:141)
+            _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2)
+            raise _tf1.no_neighbour_error()
+        (W1, b1, W2, b2), _ = _tf1.gpu_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], models, alphas)
         _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2)
         return _tf1.squeeze_out(W1, b1, W2, b2)

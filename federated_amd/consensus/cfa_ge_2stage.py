@@ -156,6 +156,10 @@ class CFA_ge_process:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved
         nbr_vec = self._round_neighbors(epoch)
+        if len(nbr_vec) == 0:  # :203-211: the publish of the unassigned result fails, is retried once, raises
+            print("Unable to save file .. retrying")
+            pause(3)
+            raise _tf1.no_neighbour_error()
         W = self._stage1_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], nbr_vec, epoch, eps_t_control)
         _tf1.publish(ii, epoch, *W)  # the MIXED model (:203-211)
         wait_for("datamat{}_{}.mat".format(ii, epoch))
@@ -183,6 +187,8 @@ class CFA_ge_process:
             _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2, epoch=epoch, loss_sample=v_loss)
             return n_W_l1, n_b_l1, n_W_l2, n_b_l2, W_l1_saved, W_l2_saved, n_l1_saved, n_l2_saved
         nbr_vec = self._round_neighbors(epoch)
+        if len(nbr_vec) == 0:  # :463 reads the result the empty neighbour loop never assigned
+            raise _tf1.no_neighbour_error()
         W = self._stage1_mix([n_W_l1, n_b_l1, n_W_l2, n_b_l2], nbr_vec, epoch, eps_t_control)
         pause(3)
         _tf1.publish(ii, epoch, n_W_l1, n_b_l1, n_W_l2, n_b_l2)  # PRE-mix model (:470-478)
