@@ -54,6 +54,8 @@ SIGNATURES = {
     "cfa_device_prepare": (_c_int, [_c_int]),
     "cfa_stream_synchronize": (_c_int, [_c_void_p]),
     "cfa_counter_fetch": (_c_int, [_c_void_p, _c_void_p, _c_void_p]),
+    "cfa_stream_signal": (_c_int, [_c_void_p, ctypes.c_uint, _c_void_p]),
+    "cfa_wait_signal": (_c_int, [_c_void_p, ctypes.c_uint, _c_void_p, ctypes.c_longlong]),
     "cfa_memcpy_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,

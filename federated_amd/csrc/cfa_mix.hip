@@ -12,6 +12,8 @@
 // staging; coefficients and bucket pointers live in the kernel arguments (SGPRs); every load of
 // a tile is issued before its first use; the fan-in N is a template parameter so the fold is
 // fully unrolled.
+#include <chrono>
+
 #include "cfa_internal.h"
 
 extern "C" int cfa_version(void) { return CFA_VERSION; }
@@ -49,6 +51,34 @@ extern "C" int cfa_counter_fetch(unsigned long long* counter, unsigned long long
   hipStream_t st = (hipStream_t)stream;
   CFA_HIP_CHECK(hipMemcpyAsync(host_dst, counter, sizeof(*counter), hipMemcpyDefault, st));
   CFA_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(*counter), st));
+  return CFA_OK;
+}
+namespace {
+// One lane stores the call's value into the caller's pinned host word; stream order puts it after
+// every earlier launch of the stream, and the release makes their results visible with it.
+__global__ void stream_signal_kernel(unsigned* word, unsigned value) {
+  __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+extern "C" int cfa_stream_signal(unsigned* word_dev, unsigned value, void* stream) {
+  if (!word_dev) return fail(CFA_E_INVALID, "null signal word");
+  stream_signal_kernel<<<1, 1, 0, (hipStream_t)stream>>>(word_dev, value);
+  return check_launch("stream_signal");
+}
+extern "C" int cfa_wait_signal(const unsigned* word_host, unsigned value, void* stream, long long spin_us) {
+  if (!word_host) return fail(CFA_E_INVALID, "null signal word");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
+    if (__atomic_load_n(word_host, __ATOMIC_ACQUIRE) == value) return CFA_OK;
+    __builtin_ia32_pause();
+    if ((i & 255) == 255 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us > 0 ? spin_us : 0))
+      break;
+  }
+  CFA_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (__atomic_load_n(word_host, __ATOMIC_ACQUIRE) != value)
+    return fail(CFA_E_INVALID, "signal word holds %u after the stream completed, expected %u",
+                __atomic_load_n(word_host, __ATOMIC_ACQUIRE), value);
   return CFA_OK;
 }
 extern "C" const char* cfa_last_error(void) { return g_last_error.c_str(); }

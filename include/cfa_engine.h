@@ -210,6 +210,16 @@ CFA_API int cfa_stream_synchronize(void* stream);
 /* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream): the staging copy of the host path. */
 CFA_API int cfa_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
 CFA_API int cfa_counter_fetch(unsigned long long* counter, unsigned long long* host_dst, void* stream);
+/* Completion of a short call without hipStreamSynchronize's wake-up: cfa_stream_signal enqueues
+ * a one-lane kernel that stores `value` into the 32-bit word `word_dev` (the device address of a
+ * pinned host word, cfa_host_device_pointer) with a system-scope release, after the stream's
+ * earlier work; cfa_wait_signal spins on the host word (acquire loads) until it reads `value`.
+ * After spin_us microseconds without it, cfa_wait_signal falls back to hipStreamSynchronize(stream),
+ * which also reports any error of the stream's work, and then requires the value. At the C1 call
+ * shape this completes 3.5 us sooner than hipStreamSynchronize (profiles/r03v_flag_sync.jsonl).
+ * The caller gives each concurrent user its own word and changes `value` at every call. */
+CFA_API int cfa_stream_signal(unsigned* word_dev, unsigned value, void* stream);
+CFA_API int cfa_wait_signal(const unsigned* word_host, unsigned value, void* stream, long long spin_us);
 
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.

@@ -72,6 +72,37 @@ def test_invalid_arguments_fail_loudly_before_any_device_work():
         _lib.call("cfa_allreduce_sum_f32", None, None, None, 4, None)
 
 
+def test_wait_signal_sees_a_word_set_by_another_thread_without_gpu():
+    """cfa_wait_signal returns as soon as its host word holds the value (acquire loads): here a
+    host thread stores it after 20 ms, inside the spin budget, so no HIP call is made. A null
+    word fails before anything else."""
+    import ctypes
+    import threading
+    import time
+
+    from federated_amd import _lib
+    lib = _lib.load()
+    word = (ctypes.c_uint * 1)(0)
+    addr = ctypes.addressof(word)
+
+    def setter():
+        time.sleep(0.02)
+        word[0] = 7
+
+    th = threading.Thread(target=setter)
+    t0 = time.perf_counter()
+    th.start()
+    rc = lib.cfa_wait_signal(addr, 7, None, 10_000_000)  # 10 s spin budget: never reached
+    th.join()
+    assert rc == 0 and word[0] == 7
+    assert time.perf_counter() - t0 < 5.0
+    assert lib.cfa_wait_signal(addr, 7, None, 0) == 0  # already set: returns on the first load
+    with pytest.raises(_lib.CFAError, match="null signal word"):
+        _lib.call("cfa_wait_signal", None, 1, None, 0)
+    with pytest.raises(_lib.CFAError, match="null signal word"):
+        _lib.call("cfa_stream_signal", None, 1, None)
+
+
 def test_single_hip_runtime_in_process():
     """libcfa must bind to the HIP runtime torch loaded (one libamdhip64 mapped)."""
     import torch  # noqa: F401

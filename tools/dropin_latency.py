@@ -11,7 +11,8 @@ Shapes:
 Beside each: the oracle's numpy restatement of the same arithmetic (oracle.tf1_mix /
 sequential_mix / tf1_compress, the reference's own expressions), and, for context, the bare
 kernel on device-resident buckets with its stream synchronisation, and a synchronisation alone.
-Usage: python tools/dropin_latency.py [--zero-copy-off]"""
+Usage: python tools/dropin_latency.py [--zero-copy-off] [--signal-off]
+(--signal-off: end each zero-copy call with hipStreamSynchronize instead of the signal word)"""
 import json
 import os
 import statistics
@@ -28,6 +29,8 @@ from oracle import cfa_oracle as O  # noqa: E402
 
 if "--zero-copy-off" in sys.argv:
     R.SINGLE_ZERO_COPY = R.TF1_ZERO_COPY = False
+if "--signal-off" in sys.argv:
+    R.SIGNAL_COMPLETION = False
 
 
 def med(fn, n=300):
@@ -44,7 +47,8 @@ def med(fn, n=300):
 rng = np.random.default_rng(0)
 mx = R.mixer()
 eng = get_engine(0)
-res = {"experiment": "tools/dropin_latency.py", "zero_copy": R.SINGLE_ZERO_COPY and R.TF1_ZERO_COPY}
+res = {"experiment": "tools/dropin_latency.py", "zero_copy": R.SINGLE_ZERO_COPY and R.TF1_ZERO_COPY,
+       "signal_completion": R.SIGNAL_COMPLETION}
 
 # C1: 2NN shapes, 2 neighbours, eps = 1, N = 2 -> alpha = eps * wf = 1/2 each (cfa.py:66-76)
 shapes = [(512, 32), (32,), (32, 8), (8,)]

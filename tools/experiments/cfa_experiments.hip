@@ -526,3 +526,177 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress(
 #undef CFA_C
   return fail(CFA_E_INVALID, "variant not instantiated");
 }
+
+// ------------------------------------------------------------------------------------------
+// Software-pipelining experiment (tools/probe/pipe_mix.py): the production mix_vec_kernel issues
+// every load of a tile, folds it, stores it, and only then issues the next tile's loads, so with
+// one wave per SIMD the memory pipe idles while a tile folds and stores. Here the loads of the
+// workgroup's NEXT tile are issued before the current tile is folded (two register sets, the loop
+// unrolled by two so no copies; branches only ahead of the loads, so each fold waits with a
+// vmcnt that leaves the next tile's loads in flight). Same loads (nt), fold and sc1 store as the
+// production kernel: the output is identical. RULE 0 sequential, 2 divisor fold.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <int N, int U>
+__device__ __forceinline__ void pipe_load(f4 (&v)[U][N + 1], const Fanin& f, long long base) {
+#pragma unroll
+  for (int k = 0; k <= N; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+  // keep the fold of the previous tile from being scheduled in between these loads (it would
+  // put a wait for the previous tile's data ahead of the remaining loads)
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N, int RULE, int U>
+__device__ __forceinline__ void pipe_fold_store(const f4 (&v)[U][N + 1], const Fanin& f,
+                                                __amdgpu_buffer_rsrc_t w, long long base) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const f4 y = fold<N, RULE>(v[u], f);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
+                                           (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+  }
+}
+template <int N, int RULE, int U>
+__global__ __launch_bounds__(kBlock) void mix_pipe_kernel(float* out, Fanin f, long long nvec) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const long long G = gridDim.x;
+  const __amdgpu_buffer_rsrc_t w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  f4 a[U][N + 1], b[U][N + 1];
+  // tiles of this workgroup: blockIdx.x + i * G for i < nt. The steady-state loop has no branch
+  // inside (a branch would merge the wait-count state of its paths and make the compiler wait
+  // for the in-flight tile at the loop head); the last one or two tiles are peeled.
+  const long long t0 = blockIdx.x;
+  const long long nt = t0 < full ? (full - 1 - t0) / G + 1 : 0;
+  const long long lane = threadIdx.x;
+  if (nt > 0) {
+    pipe_load<N, U>(a, f, t0 * kTile + lane);
+    long long i = 0;
+    for (; i + 2 < nt; i += 2) {
+      pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
+      pipe_load<N, U>(a, f, (t0 + (i + 2) * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
+    }
+    if (nt - i == 2) {
+      pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
+    } else {
+      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+      st4<false>(out, i, fold<N, RULE>(v, f));
+    }
+  }
+}
+}  // namespace
+
+// rule 0: w <- w + c_j (x_j - w); rule 2: w <- w + (c_j (x_j - w)) / d_j. n = 8 only (the
+// headline fan-in); P % 4 == 0 and P * 4 < 2 GiB (one buffer-store range).
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix_pipe(
+    float* out, const float* local, const float* const* nbrs, const float* coeff, const float* divisors,
+    size_t P, int rule, int u, int blocks_per_cu, void* stream) {
+  if (P % 4 || P * 4 > 0x7ffffff0ull || !out || !local || !nbrs || !coeff)
+    return fail(CFA_E_INVALID, "pipe experiment: P %% 4, P * 4 < 2 GiB, non-null buffers");
+  Fanin f{};
+  f.src[0] = local;
+  f.d[0] = 1.0f;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = coeff[j];
+    f.d[j + 1] = divisors ? divisors[j] : 1.0f;
+  }
+  set_reciprocals(f, 8);
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * u), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_P(R, U) \
+  if (rule == R && u == U) { mix_pipe_kernel<8, R, U><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix_pipe"); }
+  CFA_P(0, 1) CFA_P(0, 2) CFA_P(0, 4) CFA_P(2, 1) CFA_P(2, 2)
+#undef CFA_P
+  return fail(CFA_E_INVALID, "pipe variant not instantiated");
+}
+
+// ------------------------------------------------------------------------------------------
+// Completion-signal experiment (tools/probe/flag_sync.py): a small zero-copy drop-in call is
+// launch + kernel + hipStreamSynchronize, and the wake-up of the blocking synchronisation is a
+// large part of its round trip. Here the completion is a sequence number written into a pinned
+// host word after the mix, and the host spins on that word:
+//   method 0: hipStreamWriteValue32 on the stream after the mix;
+//   method 1: a one-lane kernel after the mix stores the word (system-scope release);
+//   fused:    the mix kernel itself: every workgroup releases its stores at system scope and
+//             counts itself in a device counter; the last one resets the counter and stores the
+//             word (cfa_experimental_mix2_flag, n = 2, the C1 shape).
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ void flag_kernel(unsigned* flag, unsigned seq) {
+  __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(kBlock) void mix2_flag_kernel(float* out, Fanin f, long long nvec,
+                                                           unsigned* counter, unsigned* flag,
+                                                           unsigned seq) {
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (long long)gridDim.x * kBlock) {
+    f4 v[3];
+#pragma unroll
+    for (int k = 0; k <= 2; ++k) v[k] = ld4<false>(f.src[k], i);
+    st4<false>(out, i, fold<2, CFA_RULE_SEQUENTIAL>(v, f));
+  }
+  // each wave waits for its own stores (system-scope release), then the workgroup counts itself
+  __atomic_thread_fence(__ATOMIC_RELEASE);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_signal(void* stream, unsigned* flag_dev,
+                                                                              unsigned seq, int method) {
+  hipStream_t st = (hipStream_t)stream;
+  if (method == 0) {
+    CFA_HIP_CHECK(hipStreamWriteValue32(st, flag_dev, seq, 0));
+    return CFA_OK;
+  }
+  flag_kernel<<<1, 1, 0, st>>>(flag_dev, seq);
+  return check_launch("flag_kernel");
+}
+
+// Spins until *flag == seq (acquire) or max_spins polls pass; 0 = seen, 1 = timed out.
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_wait_flag(const unsigned* flag, unsigned seq,
+                                                                                 long long max_spins) {
+  for (long long i = 0; i < max_spins; ++i) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+    __builtin_ia32_pause();
+  }
+  return 1;
+}
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix2_flag(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
+    unsigned* counter_dev, unsigned* flag_dev, unsigned seq, void* stream) {
+  if (P % 4 || !out || !local || !nbrs) return fail(CFA_E_INVALID, "mix2_flag: P %% 4, null buffers");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 2; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  const unsigned grid = (unsigned)std::min<long long>((nvec + kBlock - 1) / kBlock, 1024);
+  mix2_flag_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(out, f, nvec, counter_dev, flag_dev, seq);
+  return check_launch("mix2_flag");
+}
