@@ -2,7 +2,8 @@
 """Per-call latency of the GPU pieces of one CFA-GE drop-in call at config 3's shapes (CNN,
 P = 1 488, 2 neighbours, 24 samples of 512 inputs): the stage-1 TF1 mix, the gradients at the
 neighbours' models (one batched launch), and the MEWMA update of model and saved states, with
-the numpy restatement of each beside it (oracle, same run). Medians over 300 calls."""
+the numpy restatement of each beside it (oracle, same run). Medians over 300 calls.
+--signal-off: end each call with hipStreamSynchronize instead of the completion word."""
 import json
 import os
 import statistics
@@ -15,6 +16,9 @@ import numpy as np  # noqa: E402
 from federated_amd.consensus import _runtime as R  # noqa: E402
 from federated_amd.consensus import _tf1_models  # noqa: E402
 from oracle import cfa_oracle as O  # noqa: E402
+
+if "--signal-off" in sys.argv:
+    R.SIGNAL_COMPLETION = False
 
 
 def med(fn, n=300):
@@ -38,7 +42,7 @@ N = 2
 states = [np.zeros(s + (N,), np.float64) for s in shapes]
 grads = [mk(np.float64), mk(np.float64)]
 mx = R.mixer()
-res = {"experiment": "tools/probe/c3_calls.py", "P": 1488, "n": 2}
+res = {"experiment": "tools/probe/c3_calls.py", "P": 1488, "n": 2, "signal_completion": R.SIGNAL_COMPLETION}
 res["stage1_mix_tf1_us"] = med(lambda: mx.mix_tf1(local, nbrs, [0.5, 0.5]))
 res["numpy_stage1_us"] = med(lambda: O.tf1_mix(local, nbrs, 1.0, [np.float64(0.5)] * 2))
 res["gradients_batched_us"] = med(lambda: _tf1_models.gradients_batched(1, x, y, nbrs, stride=5))
