@@ -208,6 +208,10 @@ class LoopbackTransport:
             done = hub._coll_done.setdefault(gen, {})
             done[self.rank] = ev
             if len(done) == self.world:
+                # every rank has read every post: drop the generation's entries (the waiting ranks
+                # hold `done` themselves), so a long run keeps no buffers alive
+                hub._coll_posts.pop(gen, None)
+                hub._coll_done.pop(gen, None)
                 hub.cv.notify_all()
             else:
                 hub._wait(lambda: len(done) == self.world, f"collective {gen} completion (rank {self.rank})")
