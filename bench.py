@@ -97,8 +97,9 @@ def parse():
                    help="PMC traffic summary (default profiles/r01_pmc_traffic.json, or "
                         "profiles/r01_window_pmc_traffic.json with --window-batch)")
     p.add_argument("--no-live-traffic", action="store_true",
-                   help="N = 1: do not measure roofline.traffic with rocprofv3 PMC passes in this run "
-                        "(the committed profiles/ value is reported instead)")
+                   help="do not measure roofline.traffic with rocprofv3 PMC passes in this run (N = 1: "
+                        "the dominant mix's bucket shape; N > 1: rank 0's ring round); the committed "
+                        "profiles/ value is reported instead")
     p.add_argument("--e2e", dest="e2e", action="store_true", default=True,
                    help="(default at N = 1) also measure the host-resident path on rank 0: the same mix with "
                         "the buckets in pinned host memory, serial H2D + mix + D2H, chunk-pipelined, and "
@@ -278,12 +279,15 @@ def load_traffic(path: str, P: int, K: int, kernel: str = None, devices_per_laun
     return None
 
 
-def live_traffic(P: int, K: int, timeout: float = 150.0):
+def live_traffic(P: int, K: int, timeout: float = 150.0, ring: int = 0):
     """HBM bytes per launch of the dominant kernel, measured in THIS run: two rocprofv3 PMC passes
     (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over a child process that
     launches the same kernel on the same bucket shape (tools/pmc_probe.py), corrected as
     MI355X_MICROARCH.md prescribes (KiB; gfx950 FETCH_SIZE counts half of a wide coalesced
-    read). Returns (bytes, note) or (None, reason) when the profiler is unavailable."""
+    read). ``ring`` = D: the probe runs the population round (D ring-window mixes) instead of
+    repeated mixes of one device, i.e. the N > 1 rank's shape, where the window's rows can be
+    re-read from the Infinity Cache. Returns (bytes, note) or (None, reason) when the profiler is
+    unavailable."""
     import glob
     import shutil
     import subprocess
@@ -298,7 +302,7 @@ def live_traffic(P: int, K: int, timeout: float = 150.0):
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             cmd = [prof, "--pmc", counter, "-d", os.path.join(d, counter), "-o", "pmc", "--output-format", "csv",
                    "--", sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), "--params", str(P),
-                   "--neighbours", str(K)]
+                   "--neighbours", str(K)] + (["--ring", str(ring)] if ring else [])
             try:
                 r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout)
             except subprocess.TimeoutExpired:
@@ -312,8 +316,9 @@ def live_traffic(P: int, K: int, timeout: float = 150.0):
             vals[counter] = statistics.median(per)
     read = 2.0 * vals["FETCH_SIZE"] * 1024.0
     write = vals["WRITE_SIZE"] * 1024.0
-    return read + write, ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run (tools/pmc_probe.py, "
-                          "median over the launches), read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB")
+    return read + write, ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run (tools/pmc_probe.py"
+                          + (f" --ring {ring}: a population round of {ring} ring-window mixes" if ring else "")
+                          + ", median over the launches), read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB")
 
 
 class TransportError(RuntimeError):
@@ -625,9 +630,10 @@ def main():
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
                 "rows_note": (f"each rank's rows are {shard_P(info, P)} elements; below about 6M elements the "
-                              "ring window's 9 rows fit the 256 MB Infinity Cache, so a mix re-reads the 8 rows it "
-                              "shares with the previous device's mix from it (DESIGN.md §5); value counts "
-                              "algorithmic bytes") if world > 1 and info["partition"] == "params" else None,
+                              "ring window's 9 rows fit the 256 MB Infinity Cache, so a mix can re-read the 8 rows "
+                              "it shares with the previous device's mix from it (DESIGN.md §5); value counts "
+                              "algorithmic bytes, and roofline.traffic (L2 misses, FETCH_SIZE / WRITE_SIZE) counts "
+                              "reads the Infinity Cache serves as well") if world > 1 and info["partition"] == "params" else None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -760,8 +766,10 @@ def main():
                 result["cpu_baseline_pool"] = cpu_baseline_pool(P, K, D, args.cpu_pool_seconds)
         else:
             result["cpu_baseline"] = None
-        if world == 1 and not args.no_live_traffic and not args.window_batch:
-            live, note = live_traffic(shard_P(info, P), K)
+        if not args.no_live_traffic and not args.window_batch:
+            # N > 1: the rank's own shape (its devices, its element slice) as a whole ring round,
+            # since short rows are partly re-read from the Infinity Cache (rows_note)
+            live, note = live_traffic(shard_P(info, P), K, ring=info["devices_per_rank"] if world > 1 else 0)
             rl = result["roofline"]
             if live is not None:
                 rl["traffic_committed"] = rl["traffic"]

@@ -14,6 +14,9 @@ import os, sys
 args = sys.argv[1:]
 d = args[args.index("-d") + 1]
 counter = args[args.index("--pmc") + 1]
+if os.environ.get("FAKE_ROCPROF_ARGV"):
+    with open(os.environ["FAKE_ROCPROF_ARGV"], "a") as fh:
+        fh.write(" ".join(args) + "\n")
 if os.environ.get("FAKE_ROCPROF_FAIL"):
     sys.exit(3)
 os.makedirs(os.path.join(d, "host", "1234"), exist_ok=True)
@@ -43,6 +46,18 @@ def test_live_traffic_reads_and_corrects_the_pmc_passes(fake_rocprof):
     # read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB; rows of one dispatch summed
     assert val == pytest.approx(2 * 439498.625 * 1024 + 97656.25 * 1024)
     assert "this run" in note
+
+
+def test_live_traffic_ring_mode_profiles_the_rank_round(fake_rocprof, monkeypatch, tmp_path):
+    """N > 1: the probe child runs the rank's ring round (--ring D) on the rank's slice length."""
+    import bench
+    argv = tmp_path / "argv.txt"
+    monkeypatch.setenv("FAKE_ROCPROF_ARGV", str(argv))
+    val, note = bench.live_traffic(3_125_000, 8, timeout=60, ring=128)
+    lines = argv.read_text().splitlines()
+    assert len(lines) == 2 and all("--params 3125000" in ln and ln.endswith("--ring 128") for ln in lines)
+    assert val == pytest.approx(2 * 439498.625 * 1024 + 97656.25 * 1024)
+    assert "--ring 128" in note
 
 
 def test_live_traffic_reports_a_failed_pass(fake_rocprof, monkeypatch):
