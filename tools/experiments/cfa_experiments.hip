@@ -700,3 +700,68 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix2_flag
   mix2_flag_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(out, f, nvec, counter_dev, flag_dev, seq);
   return check_launch("mix2_flag");
 }
+
+// ------------------------------------------------------------------------------------------
+// Cache-policy experiment at the round-2 launch shape (tools/probe/policy_shape.py): round 1 chose
+// the streaming policy (nt loads, sc1 store) with 4 float4 per lane and two workgroups per CU;
+// the production default is now one workgroup per CU with 2 float4 per lane. The N = 8 mix through
+// buffer loads / stores with explicit policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1), U float4 per
+// lane, same fold: the output is identical to production.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void mix8_pol_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8;
+  const unsigned bytes = (unsigned)(nvec * 16);
+  __amdgpu_buffer_rsrc_t r[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc((void*)f.src[k], 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, bytes, 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const int base = (int)((t * kTile + threadIdx.x) * 16);
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r[k], base + u * kBlock * 16, 0, LAUX));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, fold<N, CFA_RULE_SEQUENTIAL>(v[u], f)), w,
+                                             base + u * kBlock * 16, 0, SAUX);
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+      st4<false>(out, i, fold<N, CFA_RULE_SEQUENTIAL>(v, f));
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_policy(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P, int u, int laux,
+    int saux, int blocks_per_cu, void* stream) {
+  if (P % 4 || P * 4 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "policy experiment: P %% 4, P * 4 < 2 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * u), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_Q(U, L, S) \
+  if (u == U && laux == L && saux == S) { mix8_pol_kernel<U, L, S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_pol"); }
+  CFA_Q(2, 2, 16) CFA_Q(2, 0, 16) CFA_Q(2, 16, 16) CFA_Q(2, 17, 16) CFA_Q(2, 18, 16) CFA_Q(2, 3, 16)
+  CFA_Q(2, 1, 16) CFA_Q(2, 2, 2) CFA_Q(2, 2, 0) CFA_Q(2, 2, 17) CFA_Q(2, 2, 18) CFA_Q(2, 2, 1)
+  CFA_Q(1, 2, 16) CFA_Q(4, 2, 16)
+#undef CFA_Q
+  return fail(CFA_E_INVALID, "policy variant not instantiated");
+}
