@@ -327,11 +327,14 @@ __device__ __forceinline__ void block_add_count(unsigned kept, unsigned long lon
 
 
 // Streaming-policy store (NT kernels): write-through with sc1, so the once-written output does
-// not leave dirty lines in the XCD's L2 (measured +3% over an nt store on the mix kernel,
-// tools/tune_cache_policy.py). Buffer stores take 32-bit offsets: the host splits a vector body
-// into launches of at most kMaxChunkVec float4 (2 GiB).
+// not leave dirty lines in the XCD's L2 (measured +3% over an nt store on the mix kernel at two
+// workgroups per CU, tools/tune_cache_policy.py); the sequential mix's one-workgroup shape of long
+// buckets stores nontemporally instead (kStoreNt, +1%, tools/probe/ab_store_r03.sh). Buffer
+// stores take 32-bit offsets: the host splits a vector body into launches of at most kMaxChunkVec
+// float4 (2 GiB).
 constexpr long long kMaxChunkVec = 1LL << 27;
 constexpr int kStoreSc1 = 16;
+constexpr int kStoreNt = 2;
 
 // Streaming store of one 16-byte vector with the sc1 write-through policy, as the headline mix
 // stores its output (kStoreSc1): through a buffer resource when every byte offset of the output

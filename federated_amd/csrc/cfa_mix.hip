@@ -93,11 +93,14 @@ namespace {
 // Vector mix kernel: tiles of kBlock*U float4 per block, grid-stride over tiles; the last
 // partial tile is handled with per-vector guards by the block that owns it.
 // ------------------------------------------------------------------------------------------
-template <int N, int RULE, int U, bool NT>
+// POL: 0 = default-policy loads and stores; 1 = nontemporal loads, output through the sc1
+// write-through buffer store; 2 = nontemporal loads and a nontemporal buffer store (the one
+// workgroup-per-CU shape of long buckets, see launch_vec_chunk).
+template <int N, int RULE, int U, int POL>
 __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, long long nvec) {
   constexpr long long kTile = (long long)kBlock * U;
   const long long full = nvec / kTile;
-  // (unused and removed by the compiler when !NT)
+  // (unused and removed by the compiler when POL == 0)
   const __amdgpu_buffer_rsrc_t w =
       __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
   for (long long t = blockIdx.x; t < full; t += gridDim.x) {
@@ -106,13 +109,14 @@ __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, lo
 #pragma unroll
     for (int k = 0; k <= N; ++k)
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u][k] = ld4<NT>(f.src[k], base + (long long)u * kBlock);
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<(POL != 0)>(f.src[k], base + (long long)u * kBlock);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const f4 y = fold<N, RULE>(v[u], f);
-      if constexpr (NT)
+      if constexpr (POL != 0)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
-                                               (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+                                               (int)((base + (long long)u * kBlock) * 16), 0,
+                                               POL == 2 ? kStoreNt : kStoreSc1);
       else
         st4<false>(out, base + (long long)u * kBlock, y);
     }
@@ -239,12 +243,12 @@ __global__ __launch_bounds__(kBlock) void compress_kernel(float* y, const float*
 // ------------------------------------------------------------------------------------------
 // Host-side dispatch.
 // ------------------------------------------------------------------------------------------
-template <int RULE, int U, bool NT>
+template <int RULE, int U, int POL>
 static void launch_vec_u(int n, unsigned grid, hipStream_t st, float* out, const Fanin& f,
                          long long nvec) {
 #define CFA_CASE(K) \
   case K:           \
-    mix_vec_kernel<K, RULE, U, NT><<<grid, kBlock, 0, st>>>(out, f, nvec); \
+    mix_vec_kernel<K, RULE, U, POL><<<grid, kBlock, 0, st>>>(out, f, nvec); \
     break;
   switch (n) {
     CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
@@ -289,15 +293,24 @@ static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, 
   cfa_launch_t shape = t;
   if (own) shape.blocks_per_cu = own_bpc;
   const unsigned grid = grid_for(tiles, shape);
+  // Store policy (round 3, tools/probe/store_form.py and ab_store_r03.sh): with the one-workgroup
+  // shape of buckets from 8M elements, a nontemporal store beats the sc1 write-through store
+  // (25M, n = 8: 150.4 vs 152.1-153.1 us); at the four-workgroup shape of shorter buckets and
+  // for the other rules' shapes the sc1 store stays ahead (3.125M: 17.8 vs 20.0 us).
+  const bool nt_store = own && shape.blocks_per_cu == 1 && nvec * 4 >= (8LL << 20) && t.nontemporal;
   if (U == 4) {
-    if (t.nontemporal) launch_vec_u<RULE, 4, true>(n, grid, st, out, f, nvec);
-    else launch_vec_u<RULE, 4, false>(n, grid, st, out, f, nvec);
+    if (t.nontemporal) launch_vec_u<RULE, 4, 1>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 4, 0>(n, grid, st, out, f, nvec);
   } else if (U == 2) {
-    if (t.nontemporal) launch_vec_u<RULE, 2, true>(n, grid, st, out, f, nvec);
-    else launch_vec_u<RULE, 2, false>(n, grid, st, out, f, nvec);
+    if constexpr (RULE == CFA_RULE_SEQUENTIAL)
+      if (nt_store) return launch_vec_u<RULE, 2, 2>(n, grid, st, out, f, nvec);
+    if (t.nontemporal) launch_vec_u<RULE, 2, 1>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 2, 0>(n, grid, st, out, f, nvec);
   } else {
-    if (t.nontemporal) launch_vec_u<RULE, 1, true>(n, grid, st, out, f, nvec);
-    else launch_vec_u<RULE, 1, false>(n, grid, st, out, f, nvec);
+    if constexpr (RULE == CFA_RULE_SEQUENTIAL)
+      if (nt_store) return launch_vec_u<RULE, 1, 2>(n, grid, st, out, f, nvec);
+    if (t.nontemporal) launch_vec_u<RULE, 1, 1>(n, grid, st, out, f, nvec);
+    else launch_vec_u<RULE, 1, 0>(n, grid, st, out, f, nvec);
   }
 }
 

@@ -765,3 +765,72 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_poli
 #undef CFA_Q
   return fail(CFA_E_INVALID, "policy variant not instantiated");
 }
+
+// ------------------------------------------------------------------------------------------
+// Store-form experiment (tools/probe/store_form.py): production loads (global, nt) with the output
+// stored as 0 = buffer store sc1 (production), 1 = global store nt, 2 = buffer store nt,
+// 3 = global store sc1, 4 = global store nt sc1 (3 and 4 as inline vector-store asm: no builtin
+// names those bits on a global store). U float4 per lane; identical output.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <int U, int MODE>
+__global__ __launch_bounds__(kBlock) void mix8_store_kernel(float* out, Fanin f, long long nvec) {
+  constexpr int N = 8;
+  const __amdgpu_buffer_rsrc_t w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f4 y = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
+      const long long i = base + (long long)u * kBlock;
+      if constexpr (MODE == 0)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w, (int)(i * 16), 0, kStoreSc1);
+      else if constexpr (MODE == 1)
+        __builtin_nontemporal_store(y, reinterpret_cast<f4*>(out) + i);
+      else if constexpr (MODE == 2)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w, (int)(i * 16), 0, 2);
+      else if constexpr (MODE == 3)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(reinterpret_cast<f4*>(out) + i), "v"(y) : "memory");
+      else
+        asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(reinterpret_cast<f4*>(out) + i), "v"(y) : "memory");
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
+      st4<false>(out, i, fold<N, CFA_RULE_SEQUENTIAL>(v, f));
+    }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_store(
+    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P, int u, int mode,
+    int blocks_per_cu, void* stream) {
+  if (P % 4 || P * 4 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "store experiment: P %% 4, P * 4 < 2 GiB");
+  Fanin f{};
+  f.src[0] = local;
+  for (int j = 0; j < 8; ++j) {
+    f.src[j + 1] = nbrs[j];
+    f.c[j + 1] = alphas[j];
+  }
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{blocks_per_cu, 4, 0};
+  const unsigned grid = grid_for(nvec / (kBlock * u), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_S(U, M) \
+  if (u == U && mode == M) { mix8_store_kernel<U, M><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix8_store"); }
+  CFA_S(2, 0) CFA_S(2, 1) CFA_S(2, 2) CFA_S(2, 3) CFA_S(2, 4) CFA_S(1, 1) CFA_S(4, 1)
+#undef CFA_S
+  return fail(CFA_E_INVALID, "store variant not instantiated");
+}

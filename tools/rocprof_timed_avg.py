@@ -6,7 +6,8 @@ settle loop, the warm-up rounds), so the --stats average over every dispatch mix
 timed region is the last `--steps` rounds, i.e. the last steps x launches-per-round dispatches:
 this averages exactly those, for comparison with the bench line's HIP-event figure.
 
-  python tools/rocprof_timed_avg.py TRACE.csv --last 2560 [--kernel mix_vec_kernel<8, 0, 4, true>]
+  python tools/rocprof_timed_avg.py TRACE.csv --last 2560 [--kernel "mix_vec_kernel<8, 0, 2, 2>"]
+(kernel names before the round-3 store-policy split read "mix_vec_kernel<8, 0, 2, true>")
 """
 import argparse
 import csv
@@ -18,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, required=True)
-    ap.add_argument("--kernel", default="mix_vec_kernel<8, 0, 2, true>")
+    ap.add_argument("--kernel", default="mix_vec_kernel<8, 0, 2, 2>")
     a = ap.parse_args()
     with open(a.trace) as fh:
         rows = [r for r in csv.DictReader(fh) if a.kernel in r["Kernel_Name"]]
