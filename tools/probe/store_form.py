@@ -35,6 +35,10 @@ st = torch.cuda.current_stream().cuda_stream
 variants = [("production", None, None, None), ("buffer_sc1", 2, 0, 1), ("global_nt", 2, 1, 1),
             ("buffer_nt", 2, 2, 1), ("global_sc1", 2, 3, 1), ("global_sc1_nt", 2, 4, 1),
             ("global_nt_u1", 1, 1, 1), ("global_nt_u4", 4, 1, 1)]
+if os.environ.get("STORE_SHAPES"):  # nt store at other launch shapes (workgroups per CU x float4 per lane)
+    variants = [("production", None, None, None), ("global_nt", 2, 1, 1), ("global_nt_b2", 2, 1, 2),
+                ("global_nt_u1_b2", 1, 1, 2), ("global_nt_u4_b2", 4, 1, 2), ("global_nt_b3", 2, 1, 3),
+                ("global_nt_u1_b4", 1, 1, 4), ("global_nt_u1_b3", 1, 1, 3), ("buffer_sc1_b2", 2, 0, 2)]
 
 
 def nbrs(i):
