@@ -547,17 +547,17 @@ __device__ __forceinline__ void pipe_load(f4 (&v)[U][N + 1], const Fanin& f, lon
   // put a wait for the previous tile's data ahead of the remaining loads)
   __builtin_amdgcn_sched_barrier(0);
 }
-template <int N, int RULE, int U>
+template <int N, int RULE, int U, int SAUX>
 __device__ __forceinline__ void pipe_fold_store(const f4 (&v)[U][N + 1], const Fanin& f,
                                                 __amdgpu_buffer_rsrc_t w, long long base) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const f4 y = fold<N, RULE>(v[u], f);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
-                                           (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
+                                           (int)((base + (long long)u * kBlock) * 16), 0, SAUX);
   }
 }
-template <int N, int RULE, int U>
+template <int N, int RULE, int U, int SAUX = kStoreSc1>
 __global__ __launch_bounds__(kBlock) void mix_pipe_kernel(float* out, Fanin f, long long nvec) {
   constexpr long long kTile = (long long)kBlock * U;
   const long long full = nvec / kTile;
@@ -576,16 +576,16 @@ __global__ __launch_bounds__(kBlock) void mix_pipe_kernel(float* out, Fanin f, l
     long long i = 0;
     for (; i + 2 < nt; i += 2) {
       pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
       pipe_load<N, U>(a, f, (t0 + (i + 2) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U, SAUX>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
     }
     if (nt - i == 2) {
       pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U, SAUX>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
     } else {
-      pipe_fold_store<N, RULE, U>(a, f, w, (t0 + i * G) * kTile + lane);
+      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
     }
   }
   if (blockIdx.x == (unsigned)(full % gridDim.x)) {
@@ -623,6 +623,11 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix_pipe(
   if (rule == R && u == U) { mix_pipe_kernel<8, R, U><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix_pipe"); }
   CFA_P(0, 1) CFA_P(0, 2) CFA_P(0, 4) CFA_P(2, 1) CFA_P(2, 2)
 #undef CFA_P
+  // rule + 10: the same with a nontemporal store
+#define CFA_PN(R, U) \
+  if (rule == R + 10 && u == U) { mix_pipe_kernel<8, R, U, kStoreNt><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix_pipe"); }
+  CFA_PN(0, 2) CFA_PN(2, 1) CFA_PN(2, 2)
+#undef CFA_PN
   return fail(CFA_E_INVALID, "pipe variant not instantiated");
 }
 

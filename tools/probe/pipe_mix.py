@@ -33,10 +33,16 @@ al, dv, on = _lib.float_array(alphas), _lib.float_array(divs), _lib.float_array(
 stacks = [(torch.empty(L, P, device="cuda").normal_(), torch.empty(L, P, device="cuda")) for _ in range(STACKS)]
 st = torch.cuda.current_stream().cuda_stream
 # (name, rule, u, blocks_per_cu); u None = production entry point
+if os.environ.get("PIPE_NT"):  # round 3 follow-up: the divisor fold with a nontemporal store
+    VARIANTS_NT = [("prod_seq", 0, None, None), ("pipe_seq_u2_b1_nt", 10, 2, 1), ("prod_div", 2, None, None),
+                   ("pipe_div_u2_b1", 2, 2, 1), ("pipe_div_u2_b1_nt", 12, 2, 1), ("pipe_div_u1_b1_nt", 12, 1, 1),
+                   ("pipe_div_u2_b2_nt", 12, 2, 2), ("pipe_div_u1_b2_nt", 12, 1, 2)]
 variants = [("prod_seq", 0, None, None), ("pipe_seq_u1_b1", 0, 1, 1), ("pipe_seq_u2_b1", 0, 2, 1),
             ("pipe_seq_u4_b1", 0, 4, 1), ("pipe_seq_u1_b2", 0, 1, 2), ("pipe_seq_u2_b2", 0, 2, 2),
             ("prod_div", 2, None, None), ("pipe_div_u1_b1", 2, 1, 1), ("pipe_div_u1_b2", 2, 1, 2),
             ("pipe_div_u2_b1", 2, 2, 1), ("pipe_div_u2_b2", 2, 2, 2)]
+if os.environ.get("PIPE_NT"):
+    variants = VARIANTS_NT
 
 
 def nbrs(m, i):
@@ -45,15 +51,16 @@ def nbrs(m, i):
 
 def mix(v, m, o, i):
     name, rule, u, bpc = v
+    base_rule = rule % 10
     if u is None:
-        if rule == 0:
+        if base_rule == 0:
             eng.mix_seq(o[i], m[i], nbrs(m, i), alphas)
         else:
             eng.mix_seq_div(o[i], m[i], nbrs(m, i), ones, divs)
         return
-    coeff = al if rule == 0 else on
+    coeff = al if base_rule == 0 else on
     rc = fn(o[i].data_ptr(), m[i].data_ptr(), _lib.ptr_table([x.data_ptr() for x in nbrs(m, i)]), coeff,
-            dv if rule == 2 else None, P, rule, u, bpc, st)
+            dv if base_rule == 2 else None, P, rule, u, bpc, st)
     assert rc == 0, lib.cfa_exp_last_error()
 
 
@@ -69,7 +76,7 @@ for v in variants:
     o0[3].zero_()
     mix(v, m0, o0, 3)
     torch.cuda.synchronize()
-    assert torch.equal(o0[3], refs[v[1]]), v
+    assert torch.equal(o0[3], refs[v[1] % 10]), v
 print(json.dumps({"check": "every variant equals its production kernel bit for bit", "P": P}), flush=True)
 
 times = {(v[0], s): [] for v in variants for s in range(STACKS)}
