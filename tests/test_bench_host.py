@@ -24,7 +24,7 @@ val = {"FETCH_SIZE": 439498.625, "WRITE_SIZE": 97656.25}[counter]
 with open(os.path.join(d, "host", "1234", "pmc_counter_collection.csv"), "w") as fh:
     fh.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
     for i in range(6):
-        name = '"void (anonymous namespace)::mix_vec_kernel<8, 0, 4, true>(float*)"'
+        name = '"void (anonymous namespace)::mix_vec_kernel<8, 0, 2, 2>(float*)"'
         fh.write(f"{i},{name},{counter},{val / 2}\n")
         fh.write(f"{i},{name},{counter},{val / 2}\n")  # per-XCD rows of one dispatch
         fh.write(f'{100 + i},"void other_kernel()",{counter},1.0\n')
