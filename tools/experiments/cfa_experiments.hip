@@ -839,3 +839,18 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_stor
 #undef CFA_S
   return fail(CFA_E_INVALID, "store variant not instantiated");
 }
+
+// Graph-replayable completion signal (tools/probe/flag_sync.py, graph variant): a device counter
+// is bumped and its new value stored into the pinned host word, so the same captured kernel
+// signals a fresh value at every replay (the host expects previous + 1).
+namespace {
+__global__ void flag_inc_kernel(unsigned* counter_dev, unsigned* flag) {
+  const unsigned v = __hip_atomic_fetch_add(counter_dev, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_signal_inc(void* stream, unsigned* counter_dev,
+                                                                                  unsigned* flag_dev) {
+  flag_inc_kernel<<<1, 1, 0, (hipStream_t)stream>>>(counter_dev, flag_dev);
+  return check_launch("flag_inc_kernel");
+}

@@ -25,7 +25,9 @@ X.cfa_experimental_wait_flag.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.
 X.cfa_experimental_mix2_flag.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint,
                                          ctypes.c_void_p]
-for fn in ("cfa_experimental_signal", "cfa_experimental_wait_flag", "cfa_experimental_mix2_flag"):
+X.cfa_experimental_signal_inc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+for fn in ("cfa_experimental_signal", "cfa_experimental_wait_flag", "cfa_experimental_mix2_flag",
+           "cfa_experimental_signal_inc"):
     getattr(X, fn).restype = ctypes.c_int
 
 
@@ -85,9 +87,30 @@ def fused():
     assert X.cfa_experimental_wait_flag(flag_host, seq[0], 1 << 34) == 0
 
 
+# graph variant: the mix and a counter-bumping signal kernel captured once, replayed per call
+gflag_t = torch.zeros(16, dtype=torch.int32, pin_memory=True)
+gflag_host, gflag_dev = gflag_t.data_ptr(), eng.host_device_ptr(gflag_t)
+gcounter = torch.zeros(16, dtype=torch.int32, device="cuda")
+gs = torch.cuda.Stream()
+torch.cuda.synchronize()
+graph = torch.cuda.CUDAGraph()
+with torch.cuda.graph(graph, stream=gs):
+    L.cfa_mix_seq_f32(plan.ob, plan.hb, plan.table, co, 2, plan.P, gs.cuda_stream)
+    X.cfa_experimental_signal_inc(gs.cuda_stream, gcounter.data_ptr(), gflag_dev)
+torch.cuda.synchronize()
+gseq = [int(gflag_t[0])]
+
+
+def graphed():
+    gseq[0] += 1
+    graph.replay()
+    assert X.cfa_experimental_wait_flag(gflag_host, gseq[0], 1 << 34) == 0
+
+
 base()
 ref = plan.out_np.copy()
-for name, fn in [("write_value32", signalled(0)), ("flag_kernel", signalled(1)), ("fused_last_block", fused)]:
+for name, fn in [("write_value32", signalled(0)), ("flag_kernel", signalled(1)), ("fused_last_block", fused),
+                 ("graph_mix_and_signal", graphed)]:
     plan.out_np[:] = 0
     L.cfa_stream_synchronize(sh)
     fn()
@@ -98,7 +121,8 @@ for name, fn in [("write_value32", signalled(0)), ("flag_kernel", signalled(1)),
 rows = {}
 for rep in range(3):
     for name, fn in [("hipStreamSynchronize", base), ("write_value32", signalled(0)),
-                     ("flag_kernel", signalled(1)), ("fused_last_block", fused)]:
+                     ("flag_kernel", signalled(1)), ("fused_last_block", fused),
+                     ("graph_mix_and_signal", graphed)]:
         rows.setdefault(name, []).append(med(fn))
         L.cfa_stream_synchronize(sh)
 for name, v in rows.items():
