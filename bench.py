@@ -9,16 +9,18 @@ a wrap-around ring window of K = 8 neighbours. One step = one consensus round of
 population.
 
 Scaling (SURVEY §8 e: "Strong scaling, fixed population"): the population stays D = 128 for
-every N. At N > 1 the headline ``value`` uses the element split SURVEY §8 e (1) names for the
-8 x 25M bucket scaling run (``--partition params``: every rank holds a 1/N slice of every
-device's bucket; elements are independent, so there is no exchange). Beside it, in
-``partitions``, the same population, steps and clock on the other partitions: ``devices``
-(contiguous device blocks, north_star's "devices sharded": a round is the routed halo exchange of
-the 2x4 boundary buckets of each rank -- federated_amd/halo.py: direct plus relayed xGMI paths,
-sent row by row -- overlapped with the interior mixes, each boundary device mixing as soon as the
-rows it reads have landed), ``hybrid2`` (from N = 4: 2 device blocks x N/2 slices) and ``weak``
-(128 devices per GPU, D = 128 N). ``--partition devices|hybrid`` makes either the headline;
-``--devices-per-gpu L`` keeps the per-GPU population fixed instead (weak scaling, D = L*N).
+every N. The headline at every N is the ``devices`` partition, north_star's "when devices are
+sharded": contiguous device blocks, one per rank; a round is the routed halo exchange of the 2x4
+boundary buckets of each rank (federated_amd/halo.py: direct plus relayed xGMI paths over RCCL,
+sent row by row) overlapped with the interior mixes, each boundary device mixing as soon as the
+rows it reads have landed. Beside it, in ``partitions``, the same population, steps and clock on
+the other partitions: ``params`` (every rank a 1/N element slice of every bucket, no exchange),
+``hybrid2`` (from N = 4: 2 device blocks x N/2 slices) and ``weak`` (128 devices per GPU,
+D = 128 N). A leg whose ring window ((K + 1) rows of the rank's slice) fits the 256 MiB Infinity
+Cache is marked ``cache_reuse: true`` and also timed with its mixes in a scattered order
+(``value_scattered``: consecutive mixes share no rows), since its algorithmic-byte rate is then
+partly served by the cache and is not an HBM fraction. ``--devices-per-gpu L`` makes the weak
+form the headline (D = L*N).
 
 Each rank's population stacks are placement-calibrated before the timed region
 (``--placement-candidates``, federated_amd/placement.py: the fastest of 4 allocations per stack,
@@ -28,14 +30,21 @@ value = algorithmic bytes of all mixes on all ranks / max-over-ranks wall time, 
 algorithmic bytes = (K + 2) * P * 4 per device mix (K neighbour reads + local read + output
 write). Inputs are resident in HBM when the timed region starts.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU; RANK/LOCAL_RANK/WORLD_SIZE from the environment).
-The transport (RCCL) is opened after the params headline, which exchanges nothing. If it cannot be
-opened, every leg that exchanges reports the error in ``partitions`` (``--allow-fallback`` runs
-them on a torch.distributed transport instead, marked non-comparable); with a headline that
-exchanges (``--partition devices|hybrid``, weak scaling) the run exits 3. A leg that does not finish
-within ``--leg-seconds`` is reported as an error and the line is printed with the legs measured so
-far.
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``. With N > 1 and no RANK/WORLD_SIZE in
+the environment the bench launches its own ranks: ``python -m torch.distributed.run --nnodes=1
+--nproc-per-node N --master-addr 127.0.0.1`` as a child process, before anything touches the GPU;
+the parent relays rank 0's JSON line and exits with the run's status. Under an external
+torch.distributed.run it runs as the rank it is given.
+
+Time: ``--total-seconds`` (default 420) bounds the whole run from the first launch: the headline
+is always measured; the extra legs, the CPU baselines, the PMC passes and the e2e leg each run
+only if the budget left covers their estimate, otherwise they are listed as ``skipped: budget``.
+
+Exit status: 0 = the line is complete; 3 = the transport the headline needs (RCCL) could not be
+opened on every rank (the line is printed with the ``params`` partition, which exchanges nothing,
+as ``value`` and ``config.headline_fallback`` saying why); 5 = the line is printed but an extra
+leg failed, ran out of its budget or lost a peer (named in ``partitions``); 124 = the watchdog
+ended a run stuck in its headline (no line). Self-launched, the parent returns the same status.
 """
 from __future__ import annotations
 
@@ -65,10 +74,10 @@ def parse():
                    help="simulated devices in the whole population (fixed for every N: strong scaling)")
     p.add_argument("--devices-per-gpu", type=int, default=None,
                    help="weak scaling instead: this many devices per GPU (population = N x this)")
-    p.add_argument("--partition", default=None, choices=["devices", "params", "hybrid"],
-                   help="params (default at N > 1, SURVEY §8 e (1)): every rank holds a 1/N element slice "
-                        "of every bucket (no exchange); devices: contiguous device blocks + routed halo "
-                        "exchange; hybrid: --device-groups blocks, each split over N/groups slices")
+    p.add_argument("--partition", default="devices", choices=["devices", "params", "hybrid"],
+                   help="the headline's partition: devices (default; contiguous device blocks + routed halo "
+                        "exchange), params (every rank a 1/N element slice of every bucket, no exchange), "
+                        "hybrid (--device-groups blocks, each split over N/groups slices)")
     p.add_argument("--device-groups", type=int, default=None)
     p.add_argument("--no-relay", action="store_true", help="halo on the direct links only")
     p.add_argument("--no-stages", action="store_true",
@@ -112,14 +121,108 @@ def parse():
     p.add_argument("--placement-release", action="store_true",
                    help="return the rejected placement candidates to the driver (then wait out its "
                         "background scrub) instead of leaving them in torch's caching allocator")
-    p.add_argument("--watchdog-seconds", type=float, default=900.0,
+    p.add_argument("--total-seconds", type=float, default=420.0,
+                   help="budget of the whole run from its first launch (0 = none): the headline always runs; "
+                        "extra legs, CPU baselines, PMC passes and the e2e leg only while the budget left covers "
+                        "their estimate (else listed as skipped: budget)")
+    p.add_argument("--watchdog-seconds", type=float, default=None,
                    help="end the run with status 124 and the phase it was in if it has not finished "
-                        "after this long (a collective that never completes; 0 = off)")
+                        "after this long (a collective that never completes; default --total-seconds + 90; "
+                        "0 = off)")
     p.add_argument("--leg-seconds", type=float, default=240.0,
-                   help="N > 1: budget of each extra leg (partitions beside the headline); a leg that "
+                   help="N > 1: cap on each extra leg's budget (the total budget left caps it too); a leg that "
                         "has not finished by then is reported as an error in the line, which is then "
-                        "printed with the legs measured so far (0 = no per-leg budget)")
+                        "printed with the legs measured so far (exit status 5; 0 = no per-leg cap)")
     return p.parse_args()
+
+
+STATUS_FILE_ENV = "CFA_BENCH_STATUS_FILE"  # self-launch: where rank 0 leaves the run's exit status
+T0_ENV = "CFA_BENCH_T0"  # self-launch: the parent's start (epoch seconds), the budget's origin
+EXIT_TRANSPORT, EXIT_LEG, EXIT_WATCHDOG = 3, 5, 124
+
+
+def record_status(code: int) -> None:
+    """Leave the run's exit status where a self-launching parent reads it (torch.distributed.run
+    itself only reports 0 or 1). The first status written wins."""
+    path = os.environ.get(STATUS_FILE_ENV)
+    if not path:
+        return
+    try:
+        fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644)
+    except OSError:
+        return
+    with os.fdopen(fd, "w") as fh:
+        fh.write(str(int(code)))
+
+
+def wait_for_status(seconds: float) -> None:
+    """A rank other than 0 about to leave early: wait until rank 0 has recorded the run's status
+    (self-launched runs), else ``seconds``, so rank 0 is not ended before its line is printed."""
+    path = os.environ.get(STATUS_FILE_ENV)
+    end = time.time() + seconds
+    while time.time() < end:
+        if path and os.path.exists(path):
+            time.sleep(0.5)  # the line is printed before the status is recorded
+            return
+        time.sleep(0.1)
+
+
+def run_origin() -> float:
+    """Epoch seconds the run started: the self-launching parent's start when there is one."""
+    try:
+        return float(os.environ[T0_ENV])
+    except (KeyError, ValueError):
+        return time.time()
+
+
+class Budget:
+    """The whole run's time budget (``--total-seconds``) from ``t0`` (epoch seconds)."""
+
+    def __init__(self, total: float, t0: float = None, clock=time.time):
+        self.total, self.clock = float(total), clock
+        self.t0 = clock() if t0 is None else float(t0)
+
+    def left(self) -> float:
+        if self.total <= 0:
+            return float("inf")
+        return self.total - (self.clock() - self.t0)
+
+    def allows(self, seconds: float) -> bool:
+        return self.left() >= seconds
+
+
+def extra_legs(world: int, devices: int, headline: str, weak_leg: bool = True):
+    """The N > 1 legs measured beside the headline, in the order they run (and are dropped when the
+    budget runs short: the last ones first): [(name, partition, device groups or None)]."""
+    legs = [(part, part, None) for part in ("devices", "params") if part != headline]
+    if world >= 4 and devices % 2 == 0 and headline != "hybrid":
+        legs.append(("hybrid2", "hybrid", 2))
+    if weak_leg:
+        legs.append(("weak", "devices", None))
+    return legs
+
+
+def leg_estimate(name: str, world: int, headline_seconds: float, scattered: bool = False) -> float:
+    """Seconds a leg is expected to take, from the headline's own build + autotune + timed rounds
+    (same population; the weak leg holds N times the devices per rank), with a 1.5x margin and a
+    second timed pass for a cache-reuse leg's scattered order."""
+    work = float(world) if name == "weak" else 1.0
+    return 1.5 * headline_seconds * work * (1.5 if scattered else 1.0)
+
+
+def plan_within_budget(legs, estimates, left: float, reserve: float):
+    """Which legs fit: walks ``legs`` in order, keeping each whose estimate fits in what is left
+    after ``reserve`` (the report's own share) and the legs kept before it. Returns (kept,
+    skipped) name lists. Host logic of the budget; at run time each leg is re-checked against the
+    clock (and agreed across ranks) just before it starts."""
+    kept, skipped = [], []
+    for (name, *_), est in zip(legs, estimates):
+        if left - reserve >= est:
+            kept.append(name)
+            left -= est
+        else:
+            skipped.append(name)
+    return kept, skipped
 
 
 class Watchdog:
@@ -128,26 +231,29 @@ class Watchdog:
     mismatched exchange) otherwise hangs every rank until an outer limit kills the job without
     saying where; torch.distributed.run tears the other ranks down once this one exits."""
 
-    def __init__(self, seconds: float, rank: int):
+    def __init__(self, seconds: float, rank: int, t0: float = None):
         import threading
         self.phase, self.rank, self._done = "start-up", rank, threading.Event()
-        self.t0 = time.perf_counter()
+        self.t0 = time.time() if t0 is None else t0
         self._leg = None  # (deadline, budget, on_expire) of a phase entered with its own budget
         self.seconds = seconds
         threading.Thread(target=self._watch, daemon=True).start()
 
     def _watch(self):
         while not self._done.wait(0.25):
-            now = time.perf_counter()
+            now = time.time()
             leg = self._leg
             if leg is not None and now > leg[0]:
                 print(f"[bench rank {self.rank}] watchdog: phase '{self.phase}' did not finish within its "
                       f"{leg[1]:.0f} s budget", file=sys.stderr, flush=True)
-                os._exit(leg[2](self.phase))
+                code = leg[2](self.phase)
+                record_status(code)
+                os._exit(code)
             if self.seconds > 0 and now - self.t0 > self.seconds:
                 print(f"[bench rank {self.rank}] FATAL: watchdog: not finished after {self.seconds:.0f} s, "
                       f"stuck in phase '{self.phase}'", file=sys.stderr, flush=True)
-                os._exit(124)
+                record_status(EXIT_WATCHDOG)
+                os._exit(EXIT_WATCHDOG)
 
     def enter(self, phase: str) -> None:
         self.phase = phase
@@ -159,13 +265,104 @@ class Watchdog:
         headline is already measured, so a leg stuck in a collective is reported in the line instead
         of losing the whole run)."""
         self.phase = phase
-        self._leg = (time.perf_counter() + budget, budget, on_expire) if budget > 0 else None
+        self._leg = (time.time() + budget, budget, on_expire) if budget > 0 else None
 
     def end_leg(self) -> None:
         self._leg = None
 
     def done(self) -> None:
         self._done.set()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def child_command(argv, n: int, port: int, python: str = None) -> list:
+    """argv of the self-launched ranks: the driver's own N > 1 form (torch.distributed.run, one
+    node, N ranks, rendezvous on 127.0.0.1) around this script with the caller's arguments."""
+    return [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def child_env(base: dict, t0: float, status_file: str) -> dict:
+    env = dict(base)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env[T0_ENV] = repr(float(t0))
+    env[STATUS_FILE_ENV] = status_file
+    env["PYTHONUNBUFFERED"] = "1"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool: dmabuf IPC only
+    return env
+
+
+def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python: str = None) -> int:
+    """Run the N ranks as a child ``torch.distributed.run`` (never an exec: the parent has not
+    touched the GPU, and exits with the child's status), relay rank 0's JSON line to stdout and
+    every other line of the child's stdout to stderr, and end the child's process group if it
+    outlives the total budget by ``grace`` seconds. Returns the run's exit status: rank 0's own
+    (status file) when it left one, else the launcher's."""
+    import signal
+    import subprocess
+    import tempfile
+    import threading
+    t0 = time.time()
+    fd, status_file = tempfile.mkstemp(prefix="cfa_bench_status_")
+    os.close(fd)
+    os.unlink(status_file)  # created by the first rank that records a status
+    cmd = child_command(argv, n, free_port(), python)
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file),
+                            start_new_session=True, text=True, bufsize=1)
+    killed = threading.Event()
+
+    def kill_group():
+        killed.set()
+        print(f"[bench] FATAL: the ranks outlived the {total_seconds:.0f} s budget by {grace:.0f} s; "
+              "ending them", file=sys.stderr, flush=True)
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                proc.wait(timeout=10)
+                return
+            except subprocess.TimeoutExpired:
+                continue
+
+    timer = None
+    if total_seconds > 0:
+        timer = threading.Timer(total_seconds + grace, kill_group)
+        timer.daemon = True
+        timer.start()
+    relayed = 0
+    for line in proc.stdout:
+        if line.startswith("{") and relayed == 0:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            relayed += 1
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if timer is not None:
+        timer.cancel()
+    status = None
+    try:
+        with open(status_file) as fh:
+            status = int(fh.read().strip())
+        os.unlink(status_file)
+    except (OSError, ValueError):
+        pass
+    if killed.is_set():
+        return EXIT_WATCHDOG
+    if status is not None:
+        return status
+    return rc if rc >= 0 else 128 - rc
 
 
 def cpu_model() -> str:
@@ -414,7 +611,7 @@ def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
 
     compute = torch.cuda.current_stream()
     comm = torch.cuda.Stream() if shard.plan.world > 1 else None
-    interior = shard.plan.interior()
+    interior = shard.interior_order()
     if not interior:
         timed_kernel = False
     first_i, last_i = (interior[0], interior[-1]) if interior else (None, None)
@@ -456,20 +653,48 @@ def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
     return elapsed, durations, launches
 
 
+INFINITY_CACHE_BYTES = 256 * 2**20  # MI355X_MICROARCH.md: Infinity Cache (L3) 256 MiB
+
+
+def window_fits_cache(slice_P: int, K: int) -> bool:
+    """Does one mix's ring window ((K + 1) input rows of ``slice_P`` fp32) fit the Infinity Cache?
+    Then consecutive mixes, which share K of those rows, can re-read them from it, and an
+    algorithmic-byte rate is partly cache-served (not an HBM fraction)."""
+    return (K + 1) * slice_P * 4 <= INFINITY_CACHE_BYTES
+
+
+def leg_slice_P(partition: str, groups, world: int, P: int) -> int:
+    """A rank's row length on a partition (the slices are 64-aligned, within 64 of this)."""
+    if partition == "params":
+        return -(-P // world)
+    if partition == "hybrid":
+        return -(-P // (world // groups))
+    return P
+
+
 def main():
     args = parse()
-    watchdog = Watchdog(args.watchdog_seconds, int(os.environ.get("RANK", "0")))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the ranks are this script's children (torch.distributed.run), started before anything
+        # here touches the GPU; this process only relays their line and status
+        sys.exit(self_launch(sys.argv[1:], args.gpus, args.total_seconds))
+    t0 = run_origin()
+    budget = Budget(args.total_seconds, t0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    wd = args.watchdog_seconds
+    if wd is None:
+        wd = args.total_seconds + 90.0 if args.total_seconds > 0 else 900.0
+    watchdog = Watchdog(wd, rank, t0)
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        print(f"[bench rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} ranks",
+              file=sys.stderr, flush=True)
     ndev = torch.cuda.device_count()
     if ndev < 1:
         sys.exit("bench.py needs a ROCm GPU")
@@ -480,28 +705,25 @@ def main():
         # bounded control-plane waits: a peer that never arrives fails the barrier instead of
         # holding every rank for torch's 30-minute default
         dist.init_process_group("gloo", rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=max(60.0, args.watchdog_seconds)))
+                                timeout=datetime.timedelta(seconds=max(60.0, wd)))
 
     from federated_amd.engine import get_engine
-    from federated_amd.population import make_ring_shard
+    from federated_amd.population import make_ring_shard, scattered_order
 
     P, K = args.params, args.neighbours
     if K % 2:
         sys.exit("--neighbours must be even (ring window K/2 per side)")
     weak = args.devices_per_gpu is not None
     D = args.devices_per_gpu * world if weak else args.devices
-    if args.partition is None:
-        # SURVEY §8 e (1): "within one bucket elements are independent => split P across G GPUs with
-        # no exchange. Used for the '8 x 25M bucket' scaling run"; the device-sharded population
-        # (with its halo exchange) is measured beside it (partitions.devices)
-        args.partition = "params" if world > 1 and not weak else "devices"
+    headline = args.partition
     eng = get_engine(device)
 
-    # The transport (RCCL) carries the halo of the device-sharded partitions only. The params
-    # headline (every rank a 1/N element slice, no exchange) needs none, so at N > 1 it is measured
-    # first and the transport is opened after it, for the legs that exchange. A transport that cannot
-    # be opened then fails those legs (an "error" entry in the line, never a silent fallback); with
-    # a headline that needs it (--partition devices|hybrid, or weak scaling) the run exits 3.
+    # The transport (RCCL) carries the halo of the device-sharded partitions. It is opened
+    # collectively before the headline (every rank takes the same decision). If it cannot be
+    # opened, the headline falls back to the params partition, which exchanges nothing, the line
+    # says so (config.headline_fallback) and the run exits 3; every leg that exchanges reports the
+    # error in the line. Never a silent substitute transport (--allow-fallback: torch.distributed,
+    # marked non-comparable).
     tstate = {"transport": None, "comparable": True, "error": None}
 
     def ensure_transport():
@@ -515,11 +737,20 @@ def main():
             tstate["error"] = str(exc)
         return tstate["transport"]
 
-    headline_exchanges = world > 1 and (args.partition != "params" or weak)
+    headline_fallback = None
+    headline_exchanges = world > 1 and (headline != "params" or weak)
     if headline_exchanges and ensure_transport() is None:
-        print(f"[bench rank {rank}] FATAL: {tstate['error']}", file=sys.stderr, flush=True)
-        dist.destroy_process_group()
-        sys.exit(3)
+        print(f"[bench rank {rank}] {tstate['error']}", file=sys.stderr, flush=True)
+        if weak:
+            print(f"[bench rank {rank}] FATAL: the weak-scaling headline needs the transport",
+                  file=sys.stderr, flush=True)
+            if rank == 0:
+                record_status(EXIT_TRANSPORT)
+            dist.barrier()
+            dist.destroy_process_group()
+            sys.exit(EXIT_TRANSPORT)
+        headline_fallback = {"wanted": headline, "measured": "params", "error": tstate["error"]}
+        headline, headline_exchanges = "params", False
 
     def build(partition, devices=None, relay=None):
         transport = tstate["transport"]
@@ -538,7 +769,6 @@ def main():
         seed_shard(shard, info, P)
         return shard, info
 
-    watchdog.enter(f"build {args.partition} shard")
     def drop_cached():
         """Between legs: with --placement-release, return cached memory to the driver (each leg's
         calibration then settles after its scrub); by default it stays in torch's cache for the
@@ -571,17 +801,35 @@ def main():
         tune["chosen"] = "relayed"
         return xshard, xinfo, tune
 
-    shard, info, autotune = build_tuned(args.partition)
+    def timed_scattered(xshard, steps):
+        """The same rounds with the interior mixes in scattered order (consecutive mixes share no
+        window rows, population.scattered_order): (max-over-ranks s, per-launch ms)."""
+        xshard.mix_order = scattered_order(xshard.plan.interior(), K)
+        try:
+            xel, xdur, _ = run_leg(args, xshard, world, steps, args.warmup)
+        finally:
+            xshard.mix_order = None
+        return xel, xdur
+
+    t_head0 = time.time()
+    watchdog.enter(f"build {headline} shard")
+    shard, info, autotune = build_tuned(headline)
     watchdog.enter("timed rounds")
     elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
-    interior = shard.plan.interior()
+    interior = shard.interior_order()
     per_launch_bytes = (K + 2) * shard.P * 4 * len(interior) // launches_per_step  # algorithmic, per launch
     avg_ms = sum(durations) / max(1, len(durations))
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     launches_timed = launches_per_step * args.steps
     route = info.get("route")
+    reuse = window_fits_cache(shard_P(info, P), K)
+    scat = None
+    if reuse and not args.window_batch and len(interior) > 1:
+        watchdog.enter("timed rounds, scattered order")
+        scat = timed_scattered(shard, args.steps)
+    t_headline = time.time() - t_head0
 
     result = None
     if rank == 0:
@@ -613,6 +861,7 @@ def main():
                 "devices_total": D,
                 "devices_per_gpu": info["devices_per_rank"],
                 "partition": info["partition"],
+                "headline_fallback": headline_fallback,
                 "device_groups": info["device_groups"],
                 "param_slices": info["param_slices"],
                 "bytes_per_device_mix": (K + 2) * P * 4,
@@ -626,14 +875,18 @@ def main():
                                   "autotune": autotune}) if route else None,
                 "placement": info.get("placement"),
                 "halo_carved": info.get("halo_carved"),
+                "cache_reuse": reuse,
+                "gpus_visible": ndev,
+                "ranks_share_gpus": world > ndev,
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
-                "rows_note": (f"each rank's rows are {shard_P(info, P)} elements; below about 6M elements the "
-                              "ring window's 9 rows fit the 256 MB Infinity Cache, so a mix can re-read the 8 rows "
-                              "it shares with the previous device's mix from it (DESIGN.md §5); value counts "
-                              "algorithmic bytes, and roofline.traffic (L2 misses, FETCH_SIZE / WRITE_SIZE) counts "
-                              "reads the Infinity Cache serves as well") if world > 1 and info["partition"] == "params" else None,
+                "rows_note": (f"each rank's rows are {shard_P(info, P)} elements, so a mix's {K + 1}-row window "
+                              f"({(K + 1) * shard_P(info, P) * 4 / 2**20:.0f} MiB) fits the 256 MiB Infinity Cache "
+                              "and consecutive mixes can re-read the rows they share from it: value counts "
+                              "algorithmic bytes, value_scattered is the same round with no two consecutive mixes "
+                              "sharing a row (DESIGN.md §5)") if reuse else None,
+                "budget": {"total_s": args.total_seconds, "headline_s": round(t_headline, 1)},
             },
             "roofline": {
                 "bound": "hbm",
@@ -648,12 +901,23 @@ def main():
                 "launches_timed": launches_timed,
                 "bytes_per_launch": per_launch_bytes,
                 "timing": "HIP events around each step's back-to-back interior mixes / launches",
+                "cache_reuse": reuse,
                 "traffic": load_traffic(
                     args.traffic_json or os.path.join(ROOT, "profiles", "r01_window_pmc_traffic.json"
                                                       if args.window_batch else "r01_pmc_traffic.json"),
                     shard_P(info, P), K, kernel, args.window_batch or 1),
             },
         }
+        if scat is not None:
+            xel, xdur = scat
+            result["value_scattered"] = round(bytes_total / xel / 1e9, 2)
+            result["ms_per_step_scattered"] = round(xel / args.steps * 1e3, 4)
+            if xdur:
+                xavg = sum(xdur) / len(xdur)
+                rl = result["roofline"]
+                rl["avg_launch_ms_scattered"] = round(xavg, 5)
+                rl["achieved_scattered"] = round(per_launch_bytes / (xavg * 1e-3) / 1e9, 1)
+                rl["frac_scattered"] = round(rl["achieved_scattered"] / HBM_PEAK_GBS, 4)
         pl = info.get("placement") or {}
         if pl.get("plain_us"):
             # the same mix on candidate pair (0, 0), the first allocation of each stack: what the
@@ -663,61 +927,75 @@ def main():
             rl["achieved_plain_alloc"] = round(plain, 1)
             rl["frac_plain_alloc"] = round(plain / HBM_PEAK_GBS, 4)
             rl["placement_rejected_cached_GiB"] = pl.get("rejected_cached_GiB")
+
+    # what the report still needs after the legs: rank 0's PMC passes (a child process each) and,
+    # at N = 1, the CPU baselines and the e2e leg
+    live = not args.no_live_traffic and not args.window_batch
+    pmc_est = 45.0
+    reserve = 15.0 + (2 * pmc_est if live else 0.0)
     legs = {}
-    if rank == 0 and world > 1 and not args.no_extra_legs and not weak:
-        result["partitions"] = legs  # filled as the legs finish (a leg over budget reports what it has)
+    leg_failed = False
     if world > 1 and not args.no_extra_legs and not weak:
         del shard
         drop_cached()
+        if rank == 0:
+            result["partitions"] = legs  # filled as the legs finish (a leg over budget reports what it has)
         notes = {
             "params": "same population and steps, every rank holds a 1/N element slice of every bucket "
                       "(SURVEY §8 e (1)); no exchange",
             "devices": "same population and steps in contiguous device blocks (north_star: devices sharded); "
                        "the routed halo of the ring window exchanged every round",
-            "hybrid": "same population and steps, 2 device blocks, each split over N/2 element slices; routed "
-                      "halo between ranks holding the same slice",
+            "hybrid2": "same population and steps, 2 device blocks, each split over N/2 element slices; routed "
+                       "halo between ranks holding the same slice",
             "weak": f"{args.devices} devices per GPU (population grown with N), devices partition",
         }
-        extra = [(part, None) for part in ("params", "devices") if part != args.partition]
-        if world >= 4 and D % 2 == 0 and args.partition != "hybrid":
-            extra.append(("hybrid", 2))
-        if not args.no_weak_leg:
-            # weak form for reference: the single-GPU population on every rank (D = 128 N) in device
-            # blocks, the routed halo hidden under 120 interior mixes per rank
-            extra.append(("weak", None))
 
         import threading
         report_lock = threading.Lock()
 
         def report_early(name, why):
             """Rank 0: print the line once, with the legs measured so far and ``name`` marked with
-            ``why`` (the headline is complete). Returns the exit status, 0."""
+            ``why`` (the headline is complete). Returns the exit status, 5. The other ranks give rank
+            0 time to print first (torch.distributed.run ends every rank once one has exited)."""
             with report_lock:
                 if rank == 0 and not report_early.done:
                     out = json.loads(json.dumps(result))
-                    out["partitions"][name] = {"error": why, "note": notes[name.rstrip("0123456789")]}
+                    out["partitions"][name] = {"error": why, "note": notes[name]}
+                    out["exit_status"] = EXIT_LEG
                     print(json.dumps(out), flush=True)
+                    record_status(EXIT_LEG)
                     report_early.done = True
-            return 0
+            if rank != 0:
+                wait_for_status(15.0)
+            return EXIT_LEG
         report_early.done = False
 
-        def leg_expired(name):
+        def leg_expired(name, seconds):
             # runs on the watchdog thread of a rank whose leg budget ran out (every rank's budget
             # starts at the same collective, so they expire together)
-            return lambda phase: report_early(name, f"did not finish within {args.leg_seconds:.0f} s (phase '{phase}')")
+            return lambda phase: report_early(name, f"did not finish within {seconds:.0f} s (phase '{phase}')")
 
-        for part, groups in extra:
-            name = part if groups is None else f"{part}{groups}"
-            watchdog.leg(f"{name} leg", args.leg_seconds, leg_expired(name))
-            leg, err = {"note": notes[part]}, None
+        for name, part, groups in extra_legs(world, D, headline, not args.no_weak_leg):
+            slice_P = leg_slice_P(part, groups, world, P)
+            est = leg_estimate(name, world, t_headline, scattered=window_fits_cache(slice_P, K))
+            if not agree_all(budget.left() - reserve >= est):
+                legs[name] = {"skipped": "budget", "estimate_s": round(est, 1),
+                              "budget_left_s": round(budget.left(), 1), "note": notes[name]}
+                continue
+            seconds = budget.left() - reserve
+            if args.leg_seconds > 0:
+                seconds = min(seconds, args.leg_seconds)
+            watchdog.leg(f"{name} leg", seconds, leg_expired(name, seconds))
+            leg, err = {"note": notes[name]}, None
             xshard = None
+            t_leg = time.time()
             try:
                 if part != "params" and ensure_transport() is None:
                     raise TransportError(tstate["error"])
                 watchdog.enter(f"{name} leg")
                 saved, args.device_groups = args.device_groups, groups
                 try:
-                    if part == "weak":
+                    if name == "weak":
                         Dw = args.devices * world
                         xshard, xinfo, xtune = build_tuned("devices", Dw)
                         leg_bytes = Dw * (K + 2) * P * 4 * args.steps
@@ -729,6 +1007,13 @@ def main():
                     args.device_groups = saved
                 xel, _, _ = run_leg(args, xshard, world, args.steps, args.warmup, timed_kernel=False)
                 leg.update({"value": round(leg_bytes / xel / 1e9, 2), "ms_per_step": round(xel / args.steps * 1e3, 4)})
+                leg_reuse = window_fits_cache(shard_P(xinfo, P), K)
+                leg["cache_reuse"] = leg_reuse
+                if leg_reuse and not args.window_batch and len(xshard.plan.interior()) > 1:
+                    watchdog.enter(f"{name} leg, scattered order")
+                    sel, _ = timed_scattered(xshard, args.steps)
+                    leg["value_scattered"] = round(leg_bytes / sel / 1e9, 2)
+                    leg["ms_per_step_scattered"] = round(sel / args.steps * 1e3, 4)
                 if xinfo.get("route"):
                     leg["halo_critical_MB"] = round(xinfo["route"]["critical_elems"] * 4 / 1e6, 1)
                     leg["halo_carved"] = xinfo.get("halo_carved")
@@ -737,6 +1022,7 @@ def main():
                 if part != "params":
                     leg["transport"] = tstate["transport"].name
                     leg["comparable"] = tstate["comparable"]
+                leg["wall_s"] = round(time.time() - t_leg, 1)
             except Exception as exc:  # reported in the line; every rank takes the same decision below
                 err = f"{type(exc).__name__}: {exc}"
                 print(f"[bench rank {rank}] {name} leg failed: {err}", file=sys.stderr, flush=True)
@@ -748,43 +1034,76 @@ def main():
             except Exception as exc:  # a peer has left (its leg budget ran out first): report and end
                 print(f"[bench rank {rank}] control plane lost a peer in the {name} leg ({exc})",
                       file=sys.stderr, flush=True)
-                os._exit(report_early(name, err or f"a rank left during the leg ({type(exc).__name__})"))
+                code = report_early(name, err or f"a rank left during the leg ({type(exc).__name__})")
+                record_status(code)
+                os._exit(code)
             if not all_ok:
-                leg = {"error": err or "failed on another rank", "note": notes[part]}
+                leg = {"error": err or "failed on another rank", "note": notes[name]}
+                leg_failed = True
             legs[name] = leg
             watchdog.end_leg()
         if rank == 0 and not legs:
             result.pop("partitions", None)
     if world > 1:
         dist.barrier()
-    # CPU baselines: rank 0, N = 1 only (bounded samples).
+    # CPU baselines: rank 0, N = 1 only (bounded samples), each only if the budget left covers it
     watchdog.enter("baselines and report")
+    skipped = []
     if rank == 0:
+        e2e = args.e2e and world == 1
+        e2e_est = 30.0 if e2e else 0.0
+        tail = e2e_est + (2 * pmc_est if live else 0.0)
+        result["cpu_baseline"] = None
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(P, K, args.cpu_seconds)
+            if budget.allows(args.cpu_seconds + 10 + tail):
+                result["cpu_baseline"] = cpu_baseline(P, K, args.cpu_seconds)
+            else:
+                skipped.append("cpu_baseline")
             if args.cpu_pool_seconds > 0:
-                result["cpu_baseline_pool"] = cpu_baseline_pool(P, K, D, args.cpu_pool_seconds)
-        else:
-            result["cpu_baseline"] = None
-        if not args.no_live_traffic and not args.window_batch:
-            # N > 1: the rank's own shape (its devices, its element slice) as a whole ring round,
-            # since short rows are partly re-read from the Infinity Cache (rows_note)
-            live, note = live_traffic(shard_P(info, P), K, ring=info["devices_per_rank"] if world > 1 else 0)
+                if budget.allows(args.cpu_pool_seconds + 20 + tail):
+                    result["cpu_baseline_pool"] = cpu_baseline_pool(P, K, D, args.cpu_pool_seconds)
+                else:
+                    skipped.append("cpu_baseline_pool")
+        if live:
+            # the dominant mix's bucket shape; on rows short enough for the Infinity Cache to re-serve
+            # (rows_note), the rank's own ring round (its devices, its element slice)
             rl = result["roofline"]
-            if live is not None:
-                rl["traffic_committed"] = rl["traffic"]
-                rl["traffic"] = round(live, 1)
-                rl["traffic_over_algorithmic"] = round(live / rl["bytes_per_launch"], 5)
-            rl["traffic_source"] = note if live is not None else f"committed profile ({note})"
-        if args.e2e and world == 1:
-            from federated_amd.staging import measure_e2e
-            result["e2e"] = measure_e2e(eng, P, K)
+            pass_s = min(150.0, (budget.left() - e2e_est - 10.0) / 2)
+            if pass_s >= 30.0:
+                live_b, note = live_traffic(shard_P(info, P), K, timeout=pass_s,
+                                            ring=info["devices_per_rank"] if world > 1 and reuse else 0)
+                if live_b is not None:
+                    rl["traffic_committed"] = rl["traffic"]
+                    rl["traffic"] = round(live_b, 1)
+                    rl["traffic_over_algorithmic"] = round(live_b / rl["bytes_per_launch"], 5)
+                rl["traffic_source"] = note if live_b is not None else f"committed profile ({note})"
+            else:
+                skipped.append("live_traffic")
+                rl["traffic_source"] = "committed profile (live PMC passes skipped: budget)"
+        if e2e:
+            if budget.allows(e2e_est):
+                from federated_amd.staging import measure_e2e
+                result["e2e"] = measure_e2e(eng, P, K)
+            else:
+                skipped.append("e2e")
+    code = EXIT_TRANSPORT if headline_fallback else (EXIT_LEG if leg_failed else 0)
+    if rank == 0:
+        result["config"]["budget"].update({"skipped": skipped, "left_s": round(budget.left(), 1)})
+        result["exit_status"] = code
         print(json.dumps(result), flush=True)
+        record_status(code)
+    if world > 1:
+        # no rank leaves before rank 0's line is out: torch.distributed.run ends every rank as soon
+        # as one exits with a non-zero status
+        watchdog.enter("final barrier")
+        dist.barrier()
     if tstate["transport"] is not None:
         tstate["transport"].close()
     if world > 1:
         dist.destroy_process_group()
     watchdog.done()
+    if code:
+        sys.exit(code)
 
 
 def rccl_version():

@@ -22,9 +22,14 @@
 //     worker touches a job list after its run returned. Late workers simply miss the run, so run()
 //     never waits for a helper that was not needed (with more helpers than free cores, waiting for
 //     every helper to wake had cost a scheduling round per run).
-//   - run()'s waits are bounded: past `timeout` the pool is marked broken, run() returns false so
-//     the caller can fail with a message instead of spinning forever, and every later run copies
-//     on its caller's thread, so the pool's job list and counters are left to the stragglers.
+//   - run()'s waits are bounded: past `timeout` the pool is marked broken and the run abandoned:
+//     no job is handed out any more (the claim counter is pushed past the list) and the run is
+//     closed, then run() waits (up to `straggler_timeout`, 10 minutes) until every helper still
+//     inside a copy has left, so that when it returns false no helper writes the caller's buffers
+//     any more and the caller may free them. Every later run copies on its caller's thread. Only
+//     if a helper is still inside a copy after `straggler_timeout` (a copy that cannot finish)
+//     does run() return with it there; the caller must then keep its buffers alive
+//     (`stragglers()` > 0).
 // Workers spin (pausing, then yielding the core) for ~50 us after each run before parking on a
 // condition variable, so the runs of one pipelined call (one per chunk, tens of microseconds
 // apart) do not pay a futex wake-up each.
@@ -83,7 +88,8 @@ class CopyPool {
   // Copies every job, on up to `threads` threads (the caller included). Returns false only when
   // the jobs or the helpers did not finish within `timeout` (the pool is then broken; see above).
   bool run(const Copy* jobs, size_t njobs, int threads,
-           std::chrono::nanoseconds timeout = std::chrono::seconds(30)) {
+           std::chrono::nanoseconds timeout = std::chrono::seconds(30),
+           std::chrono::nanoseconds straggler_timeout = std::chrono::minutes(10)) {
     if (njobs == 0) return true;
     std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
     const int want = int(std::min<size_t>(size_t(std::clamp(threads, 1, kMaxThreads)), njobs));
@@ -103,12 +109,18 @@ class CopyPool {
     cv_.notify_all();
     drain(jobs_);
     const auto t0 = std::chrono::steady_clock::now();
-    if (!wait([&] { return done_.load(std::memory_order_acquire) == njobs; }, t0, timeout)) return false;
+    if (!wait([&] { return done_.load(std::memory_order_acquire) == njobs; }, t0, timeout))
+      return abandon(straggler_timeout);
     close();
-    return wait([&] { return active_.load(std::memory_order_seq_cst) == 0; }, t0, timeout);
+    if (!wait([&] { return active_.load(std::memory_order_seq_cst) == 0; }, t0, timeout))
+      return abandon(straggler_timeout);
+    return true;
   }
 
   bool broken() const { return broken_.load(std::memory_order_relaxed); }
+  // Helpers still inside a copy of an abandoned run (0 once run() has returned, unless a copy
+  // outlived straggler_timeout).
+  int stragglers() const { return active_.load(std::memory_order_acquire); }
   int workers() const { return int(workers_.size()); }
   uint64_t generation() const { return state_.load(std::memory_order_relaxed) >> 8; }
 
@@ -143,6 +155,18 @@ class CopyPool {
       }
     }
     return true;
+  }
+
+  // The run timed out (the pool is already marked broken): hand out no more jobs, take no more
+  // helpers, and wait until the helpers inside a copy have left. Returns false (the run failed).
+  bool abandon(std::chrono::nanoseconds straggler_timeout) {
+    next_.store(size_t(1) << 62, std::memory_order_seq_cst);  // every later claim is past the list
+    close();
+    const auto t1 = std::chrono::steady_clock::now();
+    while (active_.load(std::memory_order_seq_cst) != 0 &&
+           std::chrono::steady_clock::now() - t1 < straggler_timeout)
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    return false;
   }
 
   // Caller holds run_mu_, so the generation cannot move while workers are created.

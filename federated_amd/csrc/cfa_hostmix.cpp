@@ -126,6 +126,10 @@ extern "C" int cfa_host_mix_f32(float* const* out_layers, const float* const* in
   std::vector<const float*> nb(size_t(std::max(n, 1)));
   auto copy_all = [&](const char* what, size_t c) -> int {
     if (pool.run(jobs.data(), jobs.size(), nthreads)) return CFA_OK;
+    // run() returns once no helper is inside a copy any more (bounded by 10 minutes)
+    if (pool.stragglers())
+      return hfail(CFA_E_HIP, "hostmix: host copy pool did not finish the %s of chunk %zu and %d helper(s) are "
+                   "still copying: the caller's buffers must not be released", what, c, pool.stragglers());
     return hfail(CFA_E_HIP, "hostmix: host copy pool did not finish the %s of chunk %zu (pool disabled; "
                  "later calls copy on the calling thread)", what, c);
   };

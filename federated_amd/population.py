@@ -96,6 +96,29 @@ class RingShardPlan:
         return sends, recvs
 
 
+def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Do the byte ranges of two tensors intersect (same device)?"""
+    if a.device != b.device or a.numel() == 0 or b.numel() == 0:
+        return False
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
+
+
+def scattered_order(devices: List[int], K: int) -> List[int]:
+    """``devices`` reordered so that consecutive mixes share no ring-window rows: a stride of
+    3 (K + 1) through the list (every mix's K + 1 input rows are disjoint from the previous two
+    mixes' rows when the list is long enough; shorter lists fall back to the largest stride that
+    keeps one mix apart). Used to time a round whose rows the Infinity Cache cannot re-serve
+    between consecutive mixes (bench.py's ``cache_reuse`` legs); the round's result is the same."""
+    n = len(devices)
+    s = 3 * (K + 1)
+    while s > 1 and n < 2 * s:
+        s //= 2
+    if s <= 1:
+        return list(devices)
+    return [devices[i] for r in range(s) for i in range(r, n, s)]
+
+
 def slice_bounds(P: int, parts: int, align: int = 64) -> List[int]:
     """Element slice bounds of a P-element bucket split in ``parts`` contiguous, ``align``-aligned
     slices (the last takes the remainder): slice p is [b[p], b[p + 1])."""
@@ -141,7 +164,7 @@ class RingPopulationShard:
 
     def __init__(self, plan: RingShardPlan, P: int, device, transport=None, engine=None,
                  dtype=torch.float32, window_batch: int = 0, route=None, rank: Optional[int] = None,
-                 stacks: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, carve: bool = True):
+                 stacks: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, carve: bool = False):
         """``window_batch`` = B > 0 mixes B consecutive devices per ``cfa_mix_window_f32`` pass,
         loading each row of their shared window once (identical results); 0 = one streaming
         mix per device.
@@ -152,10 +175,12 @@ class RingPopulationShard:
         ``rank`` is this shard's global rank in that plan (default ``plan.rank``).
 
         ``stacks`` = (models, mixed): caller-allocated ``[L, P]`` stacks (e.g. placement-calibrated,
-        ``federated_amd.placement``) instead of fresh ones. With ``carve`` the halo rows and the
-        relay slots are cut from the spare part of the models stack's allocation when it has room
-        (``placement.spare_view``: a calibrated stack heads an allocation of 16 GiB or more), so
-        they share its placement; otherwise they are allocated on their own."""
+        ``federated_amd.placement``) instead of fresh ones. ``carve`` (only for stacks from
+        ``placement.calibrated_stacks``, which heads an allocation of 16 GiB or more with the
+        models stack; ``make_ring_shard`` sets it) cuts the halo rows and the relay slots from the
+        spare part of the models stack's allocation, so they share its placement. A carve that
+        would overlap the ``mixed`` stack (stacks cut from one caller allocation) is refused and
+        the halo is allocated on its own, as it is without ``carve``."""
         if window_batch and not (1 <= window_batch <= 8 and plan.hl <= 4 and plan.hr <= 4):
             raise ValueError("window_batch must be 1..8 with at most 4 neighbours per side")
         self.window_batch = int(window_batch)
@@ -180,6 +205,8 @@ class RingPopulationShard:
         if stacks is not None and carve and plan.world > 1:
             from .placement import spare_view
             carved = spare_view(self.models, [(plan.hl, self.P), (plan.hr, self.P), (2, max(slot, 1))])
+            if carved is not None and any(_overlaps(v, self.mixed) for v in carved):
+                carved = None
         if carved is not None:
             self.halo = {"left": carved[0], "right": carved[1]}
             self._relay_buf = carved[2]
@@ -195,6 +222,9 @@ class RingPopulationShard:
         self.alphas = [1.0 / (plan.K + 1)] * plan.K
         self._route_plan = route
         self._routed = None
+        # order of the interior mixes within a round (None: ascending device id, the ring order);
+        # the mixes write a separate stack, so any order gives the same round
+        self.mix_order: Optional[List[int]] = None
         self._launch = {}
         # stage after which each boundary device can mix (the latest stage of the halo rows it reads)
         self._ready = {}
@@ -251,6 +281,10 @@ class RingPopulationShard:
                                                               self.alphas)
         fn(stream)
 
+    def interior_order(self) -> List[int]:
+        """The interior devices in the order a round mixes them."""
+        return list(self.mix_order) if self.mix_order is not None else self.plan.interior()
+
     def window_passes(self, devices: List[int]) -> List[List[int]]:
         """Runs of consecutive local devices, cut into passes of at most window_batch."""
         passes, run = [], []
@@ -301,7 +335,7 @@ class RingPopulationShard:
         cs = compute_stream or torch.cuda.current_stream(self.device)
         routed = self.routed() if self.plan.world > 1 else None
         if routed is None:
-            self._mix_set(self.plan.interior(), cs, timer)
+            self._mix_set(self.interior_order(), cs, timer)
             self._mix_set(self.plan.boundary(), cs)
             return
         ms = comm_stream or cs
@@ -317,7 +351,7 @@ class RingPopulationShard:
                 events[stage] = ev
 
         routed.run(ms, landed)
-        self._mix_set(self.plan.interior(), cs, timer)
+        self._mix_set(self.interior_order(), cs, timer)
         for stage, devs in sets:
             ev = events.get(stage)
             if ev is not None:
@@ -369,7 +403,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                                                      dtype=dtype, release=placement_release)
         stacks = (models, mixed)
     shard = RingPopulationShard(plan, Pr, device, transport, engine, dtype, window_batch, route=route, rank=rank,
-                                stacks=stacks)
+                                stacks=stacks, carve=stacks is not None)
     info = {"partition": partition, "device_groups": gd, "param_slices": gp,
             "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L,
             "placement": placement, "halo_carved": shard.carved}

@@ -195,6 +195,10 @@ CFA_API const cfa_npy_array_t* cfa_npy_arrays(const cfa_npy_t* npy);
  * when divisors is NULL, else cfa_mix_seq_div_f32, so the result equals the single-shot mix
  * bit for bit. in_layers is model-major: model m (0 = local), layer k at
  * [m * L + k]. Returns when every output layer is written.
+ * On an error return no kernel of the call is still running (the stream is drained), and the
+ * host copy threads have left the caller's arrays, so they may be released; the one exception is
+ * a host copy that has not finished 10 minutes after the pool's 30 s limit (the message says
+ * "still copying"): the arrays passed to that call must then be kept alive.
  * cfa_host_mix_staging_elems gives the staging size one call needs. */
 CFA_API size_t cfa_host_mix_staging_elems(const size_t* layer_elems, int L, int n, size_t chunk_elems);
 CFA_API int cfa_host_mix_f32(float* const* out_layers, const float* const* in_layers,

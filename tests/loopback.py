@@ -36,7 +36,7 @@ from typing import Callable, List, Optional, Sequence
 
 import torch
 
-from . import _lib
+from federated_amd import _lib
 
 Transfer = tuple  # (contiguous fp32 CUDA tensor, peer rank)
 

@@ -122,8 +122,9 @@ int main(int argc, char** argv) {
     std::vector<cfa::Copy> jobs;
     for (size_t o = 0; o < big_src.size(); o += kBig) jobs.push_back({big_dst.data() + o, big_src.data() + o, kBig});
     const bool ok = pool.run(jobs.data(), jobs.size(), 8, std::chrono::nanoseconds(0));
-    // wait for stragglers of the timed-out run through the destructor's join below; meanwhile
-    // the pool must serve complete runs on other buffers
+    // a timed-out run returns only once no helper is inside a copy of its buffers any more
+    if (!ok && pool.stragglers() != 0) fail("timed-out run returned with helpers still copying", -1);
+    // meanwhile the pool must serve complete runs on other buffers
     for (long r = 0; r < 200; ++r) one_run(pool, b, rng, r, 4);
     std::printf("phase 3: zero-timeout run %s, pool %s\n", ok ? "completed" : "timed out",
                 pool.broken() ? "broken (serial fallback)" : "healthy");

@@ -107,3 +107,126 @@ def test_watchdog_leg_budget_reports_and_exits_with_its_status():
     ok = subprocess.run([sys.executable, "-c", code % (ROOT, 0.5, 0.1, 1.0)], capture_output=True, text=True,
                         timeout=60)
     assert ok.returncode == 0 and "finished" in ok.stdout and "partial" not in ok.stdout
+
+
+# ---- N > 1 self-launch and the total budget (round 4) ----
+
+def test_child_command_is_the_drivers_torchrun_form():
+    import bench
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    cmd = bench.child_command(argv, 8, 29555, python="/usr/bin/python3")
+    assert cmd[:3] == ["/usr/bin/python3", "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    script = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[script + 1:] == argv  # the caller's arguments, unchanged, after the script
+
+
+def test_child_env_sets_origin_and_status_and_drops_rank_vars():
+    import bench
+    base = {"PATH": "/bin", "RANK": "3", "WORLD_SIZE": "8", "LOCAL_RANK": "3", "MASTER_PORT": "1",
+            "HSA_ENABLE_IPC_MODE_LEGACY": "0", "OMP_NUM_THREADS": "16"}
+    env = bench.child_env(base, 1234.5, "/tmp/status")
+    assert "RANK" not in env and "WORLD_SIZE" not in env and "LOCAL_RANK" not in env and "MASTER_PORT" not in env
+    assert env[bench.T0_ENV] == "1234.5" and env[bench.STATUS_FILE_ENV] == "/tmp/status"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["OMP_NUM_THREADS"] == "16"
+    assert env["PYTHONUNBUFFERED"] == "1"
+    assert bench.child_env({}, 0.0, "x")["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+FAKE_TORCHRUN = r'''#!/usr/bin/env python3
+import os, sys, time
+# stand-in for "python -m torch.distributed.run ... bench.py ARGS": prints what the ranks print
+assert sys.argv[1:3] == ["-m", "torch.distributed.run"], sys.argv
+mode = os.environ.get("FAKE_MODE", "ok")
+print("[rank 1] some stdout chatter", flush=True)
+if mode == "hang":
+    time.sleep(60)
+print('{"metric": "m", "value": 1.0, "n_gpus": 2, "exit_status": %d}' % (5 if mode == "leg" else 0), flush=True)
+print('{"second": "line"}', flush=True)
+if mode == "leg":
+    with open(os.environ["CFA_BENCH_STATUS_FILE"], "w") as fh:
+        fh.write("5")
+    sys.exit(1)  # torch.distributed.run reports a failed rank as 1
+sys.exit(0)
+'''
+
+
+def _self_launch(tmp_path, mode, total=60.0, grace=120.0):
+    import subprocess
+    fake = tmp_path / "fakepy"
+    fake.write_text(FAKE_TORCHRUN)
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    code = ("import sys; sys.path.insert(0, %r); import bench\n"
+            "sys.exit(bench.self_launch(['--gpus', '2'], 2, %s, grace=%s, python=%r))" % (ROOT, total, grace, str(fake)))
+    env = dict(os.environ, FAKE_MODE=mode)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+
+
+def test_self_launch_relays_exactly_one_line_and_the_status(tmp_path):
+    import json
+    r = _self_launch(tmp_path, "ok")
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == 0 and len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
+    assert "some stdout chatter" in r.stderr and '"second"' in r.stderr and "launching 2 ranks" in r.stderr
+    # rank 0's own status (status file) wins over torch.distributed.run's 1
+    r = _self_launch(tmp_path, "leg")
+    assert r.returncode == 5 and json.loads(r.stdout.strip())["exit_status"] == 5
+
+
+def test_self_launch_ends_ranks_that_outlive_the_budget(tmp_path):
+    import time as _t
+    t = _t.time()
+    r = _self_launch(tmp_path, "hang", total=1.0, grace=1.0)
+    assert r.returncode == 124 and _t.time() - t < 30
+    assert "outlived" in r.stderr and r.stdout.strip() == ""
+
+
+def test_budget_and_leg_plan_drop_the_last_legs_first():
+    import bench
+    clock = [100.0]
+    b = bench.Budget(420, t0=100.0, clock=lambda: clock[0])
+    assert b.left() == 420 and b.allows(420) and not b.allows(421)
+    clock[0] = 400.0
+    assert b.left() == 120
+    assert bench.Budget(0, t0=0.0).left() == float("inf")
+    legs = bench.extra_legs(8, 128, "devices")
+    assert [n for n, *_ in legs] == ["params", "hybrid2", "weak"]
+    assert legs[1] == ("hybrid2", "hybrid", 2) and legs[2] == ("weak", "devices", None)
+    assert [n for n, *_ in bench.extra_legs(2, 128, "devices")] == ["params", "weak"]
+    assert [n for n, *_ in bench.extra_legs(4, 128, "params", weak_leg=False)] == ["devices", "hybrid2"]
+    est = [bench.leg_estimate(n, 8, 20.0, scattered=(n != "weak")) for n, *_ in legs]
+    assert est[0] == pytest.approx(45.0) and est[2] == pytest.approx(240.0)
+    kept, skipped = bench.plan_within_budget(legs, est, left=170.0, reserve=105.0)
+    assert kept == ["params"] and skipped == ["hybrid2", "weak"]
+    kept, skipped = bench.plan_within_budget(legs, est, left=400.0, reserve=105.0)
+    assert kept == ["params", "hybrid2"] and skipped == ["weak"]
+    kept, skipped = bench.plan_within_budget(legs, est, left=1000.0, reserve=105.0)
+    assert kept == ["params", "hybrid2", "weak"] and skipped == []
+
+
+def test_cache_reuse_marking_by_slice_size():
+    import bench
+    # N = 8 params slice (3.125M fp32 rows): 9 rows = 112.5 MB fit the 256 MiB Infinity Cache
+    assert bench.window_fits_cache(bench.leg_slice_P("params", None, 8, 25_000_000), 8)
+    # hybrid2 at N = 8 (4 slices of 6.25M): 225 MB, fits; at N = 4 (2 slices of 12.5M): does not
+    assert bench.window_fits_cache(bench.leg_slice_P("hybrid", 2, 8, 25_000_000), 8)
+    assert not bench.window_fits_cache(bench.leg_slice_P("hybrid", 2, 4, 25_000_000), 8)
+    # the devices headline keeps whole 25M buckets: 900 MB windows, no reuse at any N
+    assert not bench.window_fits_cache(bench.leg_slice_P("devices", None, 8, 25_000_000), 8)
+
+
+def test_bench_defaults_put_the_devices_partition_in_the_headline(monkeypatch):
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    a = bench.parse()
+    assert a.partition == "devices" and a.total_seconds == 420.0 and a.watchdog_seconds is None
+
+
+def test_record_status_first_writer_wins(tmp_path, monkeypatch):
+    import bench
+    path = tmp_path / "st"
+    monkeypatch.setenv(bench.STATUS_FILE_ENV, str(path))
+    bench.record_status(5)
+    bench.record_status(0)
+    assert path.read_text() == "5"

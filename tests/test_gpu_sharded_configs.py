@@ -43,7 +43,7 @@ def _c4_lists(topology, D, K):
 @pytest.mark.parametrize("topology", ["kregular_v3", "random_choice"])
 def test_c4_sharded_4_ranks_loopback(gpu, topology):
     from federated_amd.graph_population import GraphPopulationShard, GraphShardPlan
-    from federated_amd.loopback import LoopbackHub, run_ranks
+    from loopback import LoopbackHub, run_ranks
     D, K, world, P, rounds = 32, 4, 4, 1_071_748, 3
     lists = _c4_lists(topology, D, K)
     full = _seed_full(D, P, 4400)
@@ -72,7 +72,7 @@ def test_c4_sharded_4_ranks_loopback(gpu, topology):
 
 def _ring_sharded(gpu, world, D, hl, hr, P, rounds, base, relay=True, staged=True, partition="devices",
                   dev_groups=None, slices=False):
-    from federated_amd.loopback import LoopbackHub, run_ranks
+    from loopback import LoopbackHub, run_ranks
     from federated_amd.population import make_ring_shard
     full = _seed_full(D, P, base)
 
@@ -145,7 +145,7 @@ def test_ring_partitions_loopback(gpu, world, partition, groups):
 def test_sharded_fedavg_4_ranks_loopback(gpu):
     """ShardedFedAvg over 4 shards: libcfa's linear pre-scaling launch on every shard, the
     loopback sum all-reduce; within the documented 1e-5 normwise of the sequential fold."""
-    from federated_amd.loopback import run_ranks
+    from loopback import run_ranks
     from federated_amd.ps_shard import ShardedFedAvg
     world, D, P = 4, 10, 262_147
     models = _seed_full(D, P, 7700)
@@ -174,7 +174,7 @@ def test_bench_plan_n8_loopback_full_bucket(gpu, partition, groups):
     slices). One sharded round over the loopback equals the unsharded population round on the same
     GPU row for row (halo rows, relay slots and slices at their full-size offsets), and two
     boundary devices of the unsharded round equal the CPU oracle."""
-    from federated_amd.loopback import LoopbackHub, run_ranks
+    from loopback import LoopbackHub, run_ranks
     from federated_amd.population import make_ring_shard
     D, world, P, h, base = 128, 8, 25_000_000, 4, 9900
     dev = torch.device("cuda")

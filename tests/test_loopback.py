@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from federated_amd.graph_population import GraphPopulationShard, GraphShardPlan
-from federated_amd.loopback import LoopbackError, LoopbackHub, run_ranks
+from loopback import LoopbackError, LoopbackHub, run_ranks
 from federated_amd.population import make_ring_shard
 from oracle.cfa_oracle import sequential_mix, tf2_kregular_v3
 

@@ -196,10 +196,43 @@ def test_ring_shard_halo_and_relay_carved_from_calibrated_stacks():
     route = RoutePlan(world, ring_transfers(world, L, h, h, P))
     big_m = torch.zeros(L * P + 2 * h * P + 2 * route.slot_elems(rank) + 1024)
     m, o = big_m[:L * P].view(L, P), torch.zeros(L, P)
-    shard = RingPopulationShard(plan, P, "cpu", stacks=(m, o), route=route, rank=rank)
+    shard = RingPopulationShard(plan, P, "cpu", stacks=(m, o), route=route, rank=rank, carve=True)
     assert shard.carved
     ptr0, ptr1 = big_m.data_ptr(), big_m.data_ptr() + big_m.numel() * 4
     for t in (shard.halo["left"], shard.halo["right"], shard.routed().relay):
         assert ptr0 + L * P * 4 <= t.data_ptr() < ptr1
-    plain = RingPopulationShard(plan, P, "cpu", stacks=(torch.zeros(L, P), o), route=route, rank=rank)
+    plain = RingPopulationShard(plan, P, "cpu", stacks=(torch.zeros(L, P), o), route=route, rank=rank, carve=True)
     assert not plain.carved and plain.routed().relay.shape[0] == 2
+    # caller stacks are not carved unless asked (the spare room may belong to someone else)
+    assert not RingPopulationShard(plan, P, "cpu", stacks=(m, o), route=route, rank=rank).carved
+
+
+def test_ring_shard_refuses_a_carve_over_the_mixed_stack():
+    """Stacks cut from ONE caller allocation (models first, mixed right after): the spare room past
+    the models stack IS the mixed stack, so a carve would alias it; the shard allocates its halo on
+    its own and a round still equals the unsharded oracle."""
+    from federated_amd.halo import RoutePlan, ring_transfers
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    L, P, h, world, rank = 8, 256, 2, 4, 1
+    plan = RingShardPlan(rank, world, L, h)
+    route = RoutePlan(world, ring_transfers(world, L, h, h, P))
+    buf = torch.zeros(2, L, P)
+    shard = RingPopulationShard(plan, P, "cpu", stacks=(buf[0], buf[1]), route=route, rank=rank, carve=True)
+    assert not shard.carved
+    lo, hi = buf[1].data_ptr(), buf[1].data_ptr() + buf[1].numel() * 4
+    for t in (shard.halo["left"], shard.halo["right"]):
+        assert not (lo <= t.data_ptr() < hi)
+
+
+def test_scattered_order_keeps_consecutive_windows_apart():
+    from federated_amd.population import scattered_order
+    K, L = 8, 128
+    order = scattered_order(list(range(L)), K)
+    assert sorted(order) == list(range(L))
+
+    def window(g):
+        return {(g + o) % L for o in range(-K // 2, K // 2 + 1)}
+
+    for a, b, c in zip(order, order[1:], order[2:]):
+        assert not window(c) & (window(a) | window(b))
+    assert scattered_order([3, 4], 8) == [3, 4]

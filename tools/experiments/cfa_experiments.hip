@@ -854,3 +854,325 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_signal_in
   flag_inc_kernel<<<1, 1, 0, (hipStream_t)stream>>>(counter_dev, flag_dev);
   return check_launch("flag_inc_kernel");
 }
+
+// ------------------------------------------------------------------------------------------
+// Round 4, the lowest roofline rows (tools/probe/lowrow_sweep.py): the fp64 divisor fold
+// (cfa_fold_f64, rule 2), the all-fp64 MEWMA (cfa_mewma_tf1_f64) and the standalone compression
+// epilogue (cfa_compress_epilogue_f32) rebuilt on the headline mix's skeleton: full tiles of
+// kBlock x U 16-byte vectors per stream walked grid-stride with no per-vector guards (the
+// partial tail handled apart by one workgroup), every load of a tile issued before its first use,
+// and a chosen store policy (SP: 0 plain global store, 1 nontemporal global store, 2 buffer store
+// nt, 3 buffer store sc1). The arithmetic is the production kernels' own, so the output must be
+// identical (the sweep checks it bit for bit).
+// ------------------------------------------------------------------------------------------
+namespace {
+typedef double xd2 __attribute__((ext_vector_type(2)));
+struct XF64Fanin {
+  const double* src[CFA_MAX_FANIN + 1];
+  double a[CFA_MAX_FANIN + 1], d[CFA_MAX_FANIN + 1], r[CFA_MAX_FANIN + 1];
+  int fast_div;
+};
+__device__ __forceinline__ double x_ddiv_rn(double a, double b, double rb, bool fast) {
+  const double aa = __builtin_fabs(a);
+  if (fast && aa >= 0x1p-900 && aa <= 0x1p900) {
+    const double q = a * rb;
+    const double r = __builtin_fma(-q, b, a);
+    return __builtin_fma(r, rb, q);
+  }
+  return a / b;
+}
+template <typename V, int SP>
+__device__ __forceinline__ void x_store(V* base, __amdgpu_buffer_rsrc_t w, long long i, V v) {
+  if constexpr (SP == 0) base[i] = v;
+  else if constexpr (SP == 1) __builtin_nontemporal_store(v, base + i);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), w, (int)(i * 16), 0,
+                                              SP == 2 ? kStoreNt : kStoreSc1);
+}
+template <bool NT, typename V>
+__device__ __forceinline__ V x_load(const V* p, long long i) {
+  if constexpr (NT) return __builtin_nontemporal_load(p + i);
+  else return p[i];
+}
+
+template <int N>
+__device__ __forceinline__ xd2 x_fold_div(const xd2 (&v)[N + 1], const XF64Fanin& f) {
+  xd2 y;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    double w = v[0][c];
+#pragma unroll
+    for (int k = 1; k <= N; ++k) w = w + x_ddiv_rn(f.a[k] * (v[k][c] - w), f.d[k], f.r[k], f.fast_div);
+    y[c] = w;
+  }
+  return y;
+}
+
+template <int N, int U, int SP>
+__global__ __launch_bounds__(kBlock) void fold64_x_kernel(double* out, XF64Fanin f, long long nvec2) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec2 / kTile;
+  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec2 * 16), 0x00020000);
+  xd2* o = reinterpret_cast<xd2*>(out);
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    xd2 v[U][N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = x_load<true>(reinterpret_cast<const xd2*>(f.src[k]), base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) x_store<xd2, SP>(o, w, base + (long long)u * kBlock, x_fold_div<N>(v[u], f));
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec2; i += kBlock) {
+      xd2 v[N + 1];
+#pragma unroll
+      for (int k = 0; k <= N; ++k) v[k] = reinterpret_cast<const xd2*>(f.src[k])[i];
+      o[i] = x_fold_div<N>(v, f);
+    }
+  }
+}
+
+// all-fp64 MEWMA (mask 0), not the initial round: s_j = rho*g_j + (1-rho)*s_j; W -= lr*(filtered ? s_j : g_j)
+struct XMewma {
+  double* W;
+  double* s[4];
+  const double* g[4];
+  double rho, one_minus_rho, lr1, lr2;
+  long long split;  // in elements
+  int filtered;
+};
+template <int N>
+__device__ __forceinline__ void x_mewma(xd2& Wv, const xd2 (&g)[N], xd2 (&s)[N], long long e0, const XMewma& a) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    double W = Wv[c];
+    const double lr = e0 + c < a.split ? a.lr1 : a.lr2;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double sv = a.rho * g[j][c] + a.one_minus_rho * s[j][c];
+      s[j][c] = sv;
+      W = W - lr * (a.filtered ? sv : g[j][c]);
+    }
+    Wv[c] = W;
+  }
+}
+template <int N, int U, int SP, bool NTL>
+__global__ __launch_bounds__(kBlock) void mewma64_x_kernel(XMewma a, long long nvec2) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec2 / kTile;
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (unsigned)(nvec2 * 16), 0x00020000);
+  __amdgpu_buffer_rsrc_t sr[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) sr[j] = __builtin_amdgcn_make_buffer_rsrc((void*)a.s[j], 0, (unsigned)(nvec2 * 16), 0x00020000);
+  xd2* W2 = reinterpret_cast<xd2*>(a.W);
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    xd2 Wv[U], g[U][N], s[U][N];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      Wv[u] = x_load<NTL>(reinterpret_cast<const xd2*>(a.W), i);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        g[u][j] = x_load<true>(reinterpret_cast<const xd2*>(a.g[j]), i);
+        s[u][j] = x_load<NTL>(reinterpret_cast<const xd2*>(a.s[j]), i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * kBlock;
+      x_mewma<N>(Wv[u], g[u], s[u], 2 * i, a);
+#pragma unroll
+      for (int j = 0; j < N; ++j) x_store<xd2, SP>(reinterpret_cast<xd2*>(a.s[j]), sr[j], i, s[u][j]);
+      x_store<xd2, SP>(W2, wr, i, Wv[u]);
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec2; i += kBlock) {
+      xd2 Wv = W2[i], g[N], s[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        g[j] = reinterpret_cast<const xd2*>(a.g[j])[i];
+        s[j] = reinterpret_cast<const xd2*>(a.s[j])[i];
+      }
+      x_mewma<N>(Wv, g, s, 2 * i, a);
+#pragma unroll
+      for (int j = 0; j < N; ++j) reinterpret_cast<xd2*>(a.s[j])[i] = s[j];
+      W2[i] = Wv;
+    }
+  }
+}
+
+template <int U, int SP, bool NTL>
+__global__ __launch_bounds__(kBlock) void compress_full_kernel(float* y, const float* ref, long long nvec,
+                                                              CompressParams cp) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, (unsigned)(nvec * 16), 0x00020000);
+  f4* y4 = reinterpret_cast<f4*>(y);
+  unsigned kept = 0;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = x_load<NTL>(reinterpret_cast<const f4*>(y), base + (long long)u * kBlock);
+      r[u] = x_load<true>(reinterpret_cast<const f4*>(ref), base + (long long)u * kBlock);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
+      x_store<f4, SP>(y4, w, base + (long long)u * kBlock, v[u]);
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 v = y4[i];
+      const f4 r = reinterpret_cast<const f4*>(ref)[i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = compress_one(v[c], r[c], cp, kept);
+      y4[i] = v;
+    }
+  }
+  block_add_count(kept, cp.kept);
+}
+}  // namespace
+
+// out = fp64 divisor fold of local and n = 4 neighbours (rule 2); u = vectors per stream per lane,
+// sp = store policy (above), bpc = workgroups per CU (0: one per tile).
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_fold64_div(
+    double* out, const double* local, const double* const* nbrs, const double* alphas, const double* divisors,
+    size_t P, int u, int sp, int bpc, void* stream) {
+  if (P % 2 || P * 8 > 0x7ffffff0ull || ((uintptr_t)out & 15)) return fail(CFA_E_INVALID, "fold64 experiment: P even, < 2 GiB, aligned");
+  XF64Fanin f{};
+  f.src[0] = local;
+  f.fast_div = 1;
+  for (int j = 1; j <= 4; ++j) {
+    f.src[j] = nbrs[j - 1];
+    f.a[j] = alphas[j - 1];
+    f.d[j] = divisors[j - 1];
+    f.r[j] = 1.0 / f.d[j];
+    if (!(f.d[j] >= 0x1p-20 && f.d[j] <= 0x1p20)) f.fast_div = 0;
+  }
+  const long long nvec2 = (long long)P / 2;
+  cfa_launch_t lc{bpc, 4, 0};
+  const unsigned grid = grid_for(std::max(1LL, nvec2 / (kBlock * u)), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_F(U, S) \
+  if (u == U && sp == S) { fold64_x_kernel<4, U, S><<<grid, kBlock, 0, st>>>(out, f, nvec2); return check_launch("fold64_x"); }
+  CFA_F(1, 0) CFA_F(1, 1) CFA_F(1, 2) CFA_F(1, 3) CFA_F(2, 0) CFA_F(2, 1) CFA_F(2, 2) CFA_F(2, 3)
+  CFA_F(4, 1) CFA_F(4, 2)
+#undef CFA_F
+  return fail(CFA_E_INVALID, "fold64 variant not instantiated");
+}
+
+// W, s[0..1] updated in place from g[0..1] (all fp64, not init); ntl = nontemporal loads of W / s.
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_mewma64(
+    double* W, double* const* s, const double* const* g, double rho, double lr1, double lr2, size_t split,
+    int filtered, size_t P, int u, int sp, int ntl, int bpc, void* stream) {
+  if (P % 2 || P * 8 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "mewma64 experiment: P even, < 2 GiB");
+  XMewma a{};
+  a.W = W;
+  for (int j = 0; j < 2; ++j) {
+    a.s[j] = s[j];
+    a.g[j] = g[j];
+  }
+  a.rho = rho;
+  a.one_minus_rho = 1.0 - rho;
+  a.lr1 = lr1;
+  a.lr2 = lr2;
+  a.split = (long long)split;
+  a.filtered = filtered;
+  const long long nvec2 = (long long)P / 2;
+  cfa_launch_t lc{bpc, 4, 0};
+  const unsigned grid = grid_for(std::max(1LL, nvec2 / (kBlock * u)), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_M(U, S, L) \
+  if (u == U && sp == S && ntl == L) { mewma64_x_kernel<2, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec2); return check_launch("mewma64_x"); }
+  CFA_M(1, 1, 1) CFA_M(1, 2, 1) CFA_M(1, 0, 0) CFA_M(2, 1, 1) CFA_M(2, 2, 1) CFA_M(2, 0, 0) CFA_M(1, 3, 1)
+  CFA_M(2, 3, 1) CFA_M(1, 3, 0) CFA_M(2, 3, 0)
+#undef CFA_M
+  return fail(CFA_E_INVALID, "mewma64 variant not instantiated");
+}
+
+// y compressed in place against ref over the whole bucket (P % 4 == 0).
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress_full(
+    float* y, const float* ref, size_t P, int mode, unsigned long long* kept, int u, int sp, int ntl, int bpc,
+    void* stream) {
+  if (P % 4 || P * 4 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "compress experiment: P %% 4, < 2 GiB");
+  CompressParams cp{};
+  if (int rc = compress_params(mode, cp)) return rc;
+  cp.cbegin = 0;
+  cp.cend = (long long)P;
+  cp.kept = kept;
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{bpc, 4, 0};
+  const unsigned grid = grid_for(std::max(1LL, nvec / (kBlock * u)), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_C(U, S, L) \
+  if (u == U && sp == S && ntl == L) { compress_full_kernel<U, S, L><<<grid, kBlock, 0, st>>>(y, ref, nvec, cp); return check_launch("compress_full"); }
+  CFA_C(2, 0, 0) CFA_C(4, 0, 0) CFA_C(8, 0, 0) CFA_C(4, 1, 1) CFA_C(4, 2, 1) CFA_C(4, 3, 0) CFA_C(2, 2, 1) CFA_C(4, 1, 0)
+#undef CFA_C
+  return fail(CFA_E_INVALID, "compress variant not instantiated");
+}
+
+// ------------------------------------------------------------------------------------------
+// Round 4: read/write-mix ceilings (tools/probe/lowrow_sweep.py --ceilings). R streams read,
+// W streams written (dst[w] may alias src[w]: in place), the lightest possible arithmetic
+// (dst[w] = src[w] + src[R - 1]), on the same skeleton and store policies as above. The best
+// variant's rate is what this hardware streams at that read:write mix, the ceiling a kernel with
+// the same mix and no compute can reach.
+// ------------------------------------------------------------------------------------------
+namespace {
+struct RwArgs {
+  const float* src[16];
+  float* dst[8];
+};
+template <int R, int W, int U, int SP, bool NTL>
+__global__ __launch_bounds__(kBlock) void rw_kernel(RwArgs a, long long nvec) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec / kTile;
+  __amdgpu_buffer_rsrc_t wr[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) wr[w] = __builtin_amdgcn_make_buffer_rsrc((void*)a.dst[w], 0, (unsigned)(nvec * 16), 0x00020000);
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 v[U][R];
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u][k] = x_load<NTL>(reinterpret_cast<const f4*>(a.src[k]), base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const f4 y = R > 1 ? v[u][w] + v[u][R - 1] : v[u][0];
+        x_store<f4, SP>(reinterpret_cast<f4*>(a.dst[w]), wr[w], base + (long long)u * kBlock, y);
+      }
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int cfa_experimental_rw(
+    const float* const* src, float* const* dst, int r, int w, size_t P, int u, int sp, int ntl, int bpc, void* stream) {
+  if (P % 4 || P * 4 > 0x7ffffff0ull || r < 1 || r > 16 || w < 1 || w > 8)
+    return fail(CFA_E_INVALID, "rw experiment: P %% 4, < 2 GiB, 1 <= r <= 16, 1 <= w <= 8");
+  RwArgs a{};
+  for (int k = 0; k < r; ++k) a.src[k] = src[k];
+  for (int k = 0; k < w; ++k) a.dst[k] = dst[k];
+  const long long nvec = (long long)P / 4;
+  cfa_launch_t lc{bpc, 4, 0};
+  const unsigned grid = grid_for(std::max(1LL, nvec / (kBlock * u)), lc);
+  hipStream_t st = (hipStream_t)stream;
+#define CFA_RW(R, W, U, S, L) \
+  if (r == R && w == W && u == U && sp == S && ntl == L) { rw_kernel<R, W, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec); return check_launch("rw"); }
+#define CFA_RW_SHAPES(R, W) \
+  CFA_RW(R, W, 1, 1, 1) CFA_RW(R, W, 2, 1, 1) CFA_RW(R, W, 4, 1, 1) CFA_RW(R, W, 2, 3, 1) CFA_RW(R, W, 4, 3, 1) \
+  CFA_RW(R, W, 2, 2, 1) CFA_RW(R, W, 4, 0, 0) CFA_RW(R, W, 2, 0, 0) CFA_RW(R, W, 4, 3, 0) CFA_RW(R, W, 1, 3, 1)
+  CFA_RW_SHAPES(1, 1) CFA_RW_SHAPES(2, 1) CFA_RW_SHAPES(5, 1) CFA_RW_SHAPES(5, 3) CFA_RW_SHAPES(9, 1)
+#undef CFA_RW_SHAPES
+#undef CFA_RW
+  return fail(CFA_E_INVALID, "rw variant not instantiated");
+}
