@@ -308,6 +308,29 @@ __device__ __forceinline__ float compress_one(float y, float ref, const Compress
   return y;
 }
 
+// The same epilogue with the mode's form fixed at compile time (KIND: 0 none, 1 sparse, 2 DPCM;
+// compress_kind maps a mode to it) and the thresholds passed in as fp32: straight-line selects
+// instead of a per-element branch tree on the runtime mode, which kept the standalone epilogue's
+// waves off the memory pipe between tiles (round 4, tools/probe/lowrow_sweep.py). The same fp32
+// operations as compress_one, so the same values and count.
+__device__ __host__ constexpr int compress_kind(int mode) {
+  return (mode == CFA_COMPRESS_SPARSE || mode == CFA_COMPRESS_SPARSE_HI) ? 1
+         : (mode == CFA_COMPRESS_SPARSE_DPCM || mode == CFA_COMPRESS_SPARSE_DPCM_HI) ? 2 : 0;
+}
+template <int KIND>
+__device__ __forceinline__ float compress_sel(float y, float ref, float thr, float rep, unsigned& kept) {
+  if constexpr (KIND == 0) {
+    ++kept;
+    return y;
+  } else {
+    const float d = KIND == 2 ? y - ref : y;
+    const bool hit = fabsf(d) < thr;
+    const float r = KIND == 2 ? ref + np_signf(d) * rep : np_signf(y) * rep;
+    kept += hit ? 0u : 1u;
+    return hit ? r : y;
+  }
+}
+
 // Block-wide sum of one counter per lane, then a single 64-bit atomic per block.
 __device__ __forceinline__ void block_add_count(unsigned kept, unsigned long long* dst) {
   __shared__ unsigned red[kBlock / 64];

@@ -158,56 +158,71 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_f64_kernel(double* out, F64Fan
 
 // Vector form of mix_tf1_f64_kernel for 16-byte-aligned buckets: each lane moves two doubles per
 // bucket per vector, U vectors per tile, every load of a tile issued before its first use, the
-// fan-in N and the rule at compile time (the runtime loop above serialises its loads).
+// fan-in N and the rule at compile time (the runtime loop above serialises its loads). The
+// headline mix's skeleton (round 4, tools/probe/lowrow_sweep.py, profiles/r04_lowrow_sweep.jsonl):
+// full tiles walked grid-stride with no per-vector guards, the partial tail done by one
+// workgroup, and the output through the sc1 write-through buffer store (Sc1Out) at two
+// workgroups per CU: the divisor fold at n = 4 went from 0.734 to 0.815 of peak on the same
+// buffers (a nontemporal store at one vector per lane: 0.789).
+template <int N, int RULE, bool STEP0F32>
+__device__ __forceinline__ d2 fold_d2(const d2 (&v)[N + 1], const F64Fanin& f, long long idx, const double* ref,
+                                      const CompressParams& cp, int compress, unsigned& kept) {
+  d2 y;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    double w = v[0][c];
+    int j = 1;
+    if constexpr (STEP0F32) {  // both operands fp32 arrays in the reference: fp32 subtraction
+      const float d = (float)v[1][c] - (float)w;
+      w = w + f.a[1] * (double)d;
+      j = 2;
+    }
+#pragma unroll
+    for (int k = 1; k <= N; ++k) {
+      if (k < j) continue;
+      if constexpr (RULE == CFA_RULE_SEQUENTIAL) w = w + f.a[k] * (v[k][c] - w);
+      else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV)
+        w = w + ddiv_rn(f.a[k] * (v[k][c] - w), f.d[k], f.r[k], f.fast_div);
+      else w = w + f.a[k] * v[k][c];
+    }
+    if (compress) {
+      const long long e = 2 * idx + c;
+      if (e >= cp.cbegin && e < cp.cend) w = compress_one_d(w, ref[e], cp, kept);
+    }
+    y[c] = w;
+  }
+  return y;
+}
+
 template <int N, int RULE, bool STEP0F32>
 __global__ __launch_bounds__(kBlock) void fold_f64_vec_kernel(double* out, F64Fanin f, long long nvec2,
                                                                const double* ref, CompressParams cp,
                                                                int compress) {
   constexpr int U = 2;
   constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec2 / kTile;
+  const Sc1Out o = sc1_out(out, nvec2 * 16);
   unsigned kept = 0;
-  for (long long t = blockIdx.x; t * kTile < nvec2; t += gridDim.x) {
-    long long idx[U];
-    bool ok[U];
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
     d2 v[U][N + 1];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      idx[u] = t * kTile + (long long)u * kBlock + threadIdx.x;
-      ok[u] = idx[u] < nvec2;
-    }
 #pragma unroll
     for (int k = 0; k <= N; ++k)
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        v[u][k] = ok[u] ? __builtin_nontemporal_load(reinterpret_cast<const d2*>(f.src[k]) + idx[u]) : d2{0.0, 0.0};
+        v[u][k] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(f.src[k]) + base + (long long)u * kBlock);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;
-      d2 y;
+      const long long i = base + (long long)u * kBlock;
+      st16_sc1(o, i, fold_d2<N, RULE, STEP0F32>(v[u], f, i, ref, cp, compress, kept));
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec2; i += kBlock) {
+      d2 v[N + 1];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        double w = v[u][0][c];
-        int j = 1;
-        if constexpr (STEP0F32) {  // both operands fp32 arrays in the reference: fp32 subtraction
-          const float d = (float)v[u][1][c] - (float)w;
-          w = w + f.a[1] * (double)d;
-          j = 2;
-        }
-#pragma unroll
-        for (int k = 1; k <= N; ++k) {
-          if (k < j) continue;
-          if constexpr (RULE == CFA_RULE_SEQUENTIAL) w = w + f.a[k] * (v[u][k][c] - w);
-          else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV)
-            w = w + ddiv_rn(f.a[k] * (v[u][k][c] - w), f.d[k], f.r[k], f.fast_div);
-          else w = w + f.a[k] * v[u][k][c];
-        }
-        if (compress) {
-          const long long e = 2 * idx[u] + c;
-          if (e >= cp.cbegin && e < cp.cend) w = compress_one_d(w, ref[e], cp, kept);
-        }
-        y[c] = w;
-      }
-      __builtin_nontemporal_store(y, reinterpret_cast<d2*>(out) + idx[u]);
+      for (int k = 0; k <= N; ++k) v[k] = reinterpret_cast<const d2*>(f.src[k])[i];
+      st16_sc1(o, i, fold_d2<N, RULE, STEP0F32>(v, f, i, ref, cp, compress, kept));
     }
   }
   if (compress) block_add_count(kept, cp.kept);

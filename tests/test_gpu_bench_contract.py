@@ -35,3 +35,58 @@ def test_bench_line_contract():
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]
     # value = all algorithmic bytes / time: consistent with ms_per_step
     assert abs(d["value"] - 16 * 10 * 1_000_000 * 4 / (d["ms_per_step"] * 1e-3) / 1e9) <= 0.01 * d["value"]
+
+
+N_GT_1_FIELDS = [("value", float), ("ms_per_step", float), ("n_gpus", int), ("exit_status", int),
+                 ("config", dict), ("roofline", dict), ("partitions", dict)]
+CONFIG_FIELDS = ["partition", "transport", "comparable", "rccl_version", "halo_route", "cache_reuse", "rows_note",
+                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback"]
+
+
+def _self_launched(extra, timeout=240):
+    """python3 bench.py --gpus 2 ... with no torch.distributed.run: bench launches its own ranks
+    (on a one-GPU box both share the card)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--params", "1000000", "--steps", "3",
+           "--warmup", "1", "--no-live-traffic", "--total-seconds", "200"] + extra
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    return r, json.loads(lines[0])
+
+
+def test_self_launched_n2_line_matches_the_documented_schema():
+    """INTEGRATION.md §5 "Fields of the N > 1 line": the devices-partition headline (rehearsed on the
+    torch transport, since RCCL refuses two ranks on one device), every documented field present,
+    the params leg beside it with its cache-reuse marking, exit status 0."""
+    r, d = _self_launched(["--transport", "torch"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    for key, typ in N_GT_1_FIELDS:
+        assert isinstance(d[key], typ), key
+    assert d["n_gpus"] == 2 and d["exit_status"] == 0 and d["scaling"] == "strong"
+    c = d["config"]
+    for key in CONFIG_FIELDS:
+        assert key in c, key
+    assert c["partition"] == "devices" and c["headline_fallback"] is None
+    assert c["transport"] == "torch-gloo" and c["comparable"] is False
+    assert set(c["halo_route"]) >= {"relay", "stages", "critical_MB", "autotune"}
+    assert set(c["budget"]) >= {"total_s", "headline_s", "left_s", "skipped"}
+    # 1M-element rows: a 9-row window fits the Infinity Cache, so the scattered rate is there too
+    assert c["cache_reuse"] is True and isinstance(d["value_scattered"], float) and c["rows_note"]
+    p = d["partitions"]["params"]
+    assert p["cache_reuse"] is True and p["value"] > 0 and p["value_scattered"] > 0
+    assert "weak" in d["partitions"]
+
+
+def test_self_launched_n2_rccl_refused_falls_back_and_exits_3():
+    """RCCL cannot open two ranks on one device: the line still comes, with the params headline,
+    config.headline_fallback naming the error, the exchanging legs' errors, and status 3."""
+    r, d = _self_launched([])
+    if d["config"]["headline_fallback"] is None:  # a node where RCCL opened: nothing to check here
+        assert r.returncode == 0
+        return
+    assert r.returncode == 3 and d["exit_status"] == 3
+    fb = d["config"]["headline_fallback"]
+    assert fb["wanted"] == "devices" and fb["measured"] == "params" and "rccl" in fb["error"]
+    assert d["config"]["partition"] == "params" and d["value"] > 0
+    assert "error" in d["partitions"]["devices"]

@@ -130,6 +130,27 @@ def test_compress_fp32_threshold_boundaries(gpu, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+def test_compress_epilogue_grid_stride_large(gpu, mode):
+    """The standalone epilogue at more full tiles than the grid has workgroups (each walks several,
+    the partial tile by one workgroup), an odd P (scalar tail), values around every threshold:
+    identical to numpy, count included (round 4 skeleton, compile-time mode form)."""
+    rng = np.random.default_rng(330 + mode)
+    P = 4_000_003
+    ref = (rng.standard_normal(P) * 1e-2).astype(np.float32)
+    y = (ref + rng.standard_normal(P).astype(np.float32) * np.float32(2e-3)) if mode in (2, 3) else \
+        (rng.standard_normal(P) * 1e-2).astype(np.float32)
+    expect = y.copy().reshape(1, -1)
+    cnt = O.tf1_compress(expect, (ref if mode in (2, 3) else y).reshape(1, -1), mode)
+    if mode == 0:
+        cnt = P  # no epilogue: every element kept
+    dy = _dev(y)
+    kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.compress(dy, _dev(ref) if mode in (2, 3) else None, mode, kept)
+    assert np.array_equal(dy.cpu().numpy(), expect.reshape(-1))
+    assert int(kept.item()) == cnt
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n", [0, 1, 3, 17])
 def test_mix_seq_compress(gpu, mode, n):
     rng = np.random.default_rng(300 + 10 * mode + n)
@@ -319,6 +340,34 @@ def test_fold_f64_rules(gpu, rule, n):
     out = torch.empty(P, dtype=torch.float64, device="cuda")
     gpu.fold_f64(out, _dev64(local), [_dev64(x) for x in xs], a, rule, d if rule == 2 else None)
     assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("rule", [0, 2])
+def test_fold_f64_grid_stride_large(gpu, rule):
+    """A bucket of more full tiles than the grid has workgroups (each workgroup walks several, the
+    partial tile and the odd last element apart), with the compression epilogue on a range that
+    starts and ends inside tiles: identical to numpy (round 4 kernel skeleton, sc1 buffer store)."""
+    rng = np.random.default_rng(1450 + rule)
+    P, n = 4_000_003, 4
+    local = rng.standard_normal(P) * 1e-3
+    xs = [local + rng.standard_normal(P) * 1e-4 for _ in range(n)]
+    a = [0.2, 0.3, 0.25, 0.1]
+    d = [4.0, 3.0, 4.0, 7.0]
+    ref = local.copy()
+    for j in range(n):
+        ref = ref + a[j] * (xs[j] - ref) / d[j] if rule == 2 else ref + a[j] * (xs[j] - ref)
+    out = torch.empty(P, dtype=torch.float64, device="cuda")
+    gpu.fold_f64(out, _dev64(local), [_dev64(x) for x in xs], a, rule, d if rule == 2 else None)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    if rule == 0:  # the TF1 entry (same kernel) with the epilogue on [cb, ce)
+        cb, ce = 1_000_001, 3_000_007
+        y = O.tf1_mix_flat(local, xs, a)
+        seg = y[cb:ce].reshape(1, -1)
+        cnt = O.tf1_compress(seg, local[cb:ce].reshape(1, -1), 3)
+        y[cb:ce] = seg.reshape(-1)
+        kept = torch.zeros(1, dtype=torch.int64, device="cuda")
+        gpu.mix_tf1_f64(out, _dev64(local), [_dev64(x) for x in xs], a, False, 3, cb, ce, kept)
+        assert np.array_equal(out.cpu().numpy(), y) and int(kept.item()) == cnt
 
 
 def test_mix_tf1_error_paths(gpu):

@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(kBlock) void compress_full_kernel(float* y, const f
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[u][c] = compress_one(v[u][c], r[u][c], cp, kept);
+      for (int c = 0; c < 4; ++c) v[u][c] = compress_sel<2>(v[u][c], r[u][c], (float)cp.thr, (float)cp.rep, kept);
       x_store<f4, SP>(y4, w, base + (long long)u * kBlock, v[u]);
     }
   }
@@ -1101,7 +1101,8 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mewma64(
 extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress_full(
     float* y, const float* ref, size_t P, int mode, unsigned long long* kept, int u, int sp, int ntl, int bpc,
     void* stream) {
-  if (P % 4 || P * 4 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "compress experiment: P %% 4, < 2 GiB");
+  if (P % 4 || P * 4 > 0x7ffffff0ull || compress_kind(mode) != 2)
+    return fail(CFA_E_INVALID, "compress experiment: P %% 4, < 2 GiB, a DPCM mode");
   CompressParams cp{};
   if (int rc = compress_params(mode, cp)) return rc;
   cp.cbegin = 0;
@@ -1121,7 +1122,7 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress_
 // ------------------------------------------------------------------------------------------
 // Round 4: read/write-mix ceilings (tools/probe/lowrow_sweep.py --ceilings). R streams read,
 // W streams written (dst[w] may alias src[w]: in place), the lightest possible arithmetic
-// (dst[w] = src[w] + src[R - 1]), on the same skeleton and store policies as above. The best
+// (dst[w] = src[w] + the sum of all R sources: no load can be dropped), on the same skeleton and store policies as above. The best
 // variant's rate is what this hardware streams at that read:write mix, the ceiling a kernel with
 // the same mix and no compute can reach.
 // ------------------------------------------------------------------------------------------
@@ -1145,12 +1146,16 @@ __global__ __launch_bounds__(kBlock) void rw_kernel(RwArgs a, long long nvec) {
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u][k] = x_load<NTL>(reinterpret_cast<const f4*>(a.src[k]), base + (long long)u * kBlock);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      f4 acc = v[u][0];  // every loaded stream feeds every store (no load can be dropped)
+#pragma unroll
+      for (int k = 1; k < R; ++k) acc = acc + v[u][k];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const f4 y = R > 1 ? v[u][w] + v[u][R - 1] : v[u][0];
+        const f4 y = R > 1 ? acc + v[u][w] : v[u][0];
         x_store<f4, SP>(reinterpret_cast<f4*>(a.dst[w]), wr[w], base + (long long)u * kBlock, y);
       }
+    }
   }
 }
 }  // namespace

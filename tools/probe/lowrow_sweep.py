@@ -102,7 +102,7 @@ def main():
         prod()
         torch.cuda.synchronize()
         ref.copy_(out)
-        variants = [("production (2 WG/CU, U=2, nt store, guarded)", prod, (2, 2))]
+        variants = [("production (2 WG/CU, U=2, sc1 buffer store, full tiles)", prod, (2, 2))]
         for bpc, u, sp in [(1, 2, 2), (2, 2, 2), (1, 2, 1), (2, 2, 1), (2, 1, 1), (4, 1, 1), (2, 2, 3),
                            (1, 4, 2), (2, 1, 2), (4, 1, 2)]:
             fn = (lambda bpc=bpc, u=u, sp=sp: call("cfa_experimental_fold64_div", vp(out.data_ptr()), vp(loc.data_ptr()),
@@ -157,7 +157,7 @@ def main():
         prod()
         torch.cuda.synchronize()
         yr, kr = y.clone(), int(kept.item())
-        variants = [("production (2 WG/CU, U=4, default policy, guarded)", prod, (2, 4))]
+        variants = [("production (2 WG/CU, U=4, default policy, compile-time mode form)", prod, (2, 4))]
         for bpc, u, sp, ntl in [(2, 4, 0, 0), (4, 4, 0, 0), (2, 8, 0, 0), (4, 2, 0, 0), (2, 4, 1, 1),
                                 (2, 4, 2, 1), (2, 4, 3, 0), (1, 8, 0, 0), (2, 4, 1, 0), (4, 4, 2, 1)]:
             fn = (lambda bpc=bpc, u=u, sp=sp, ntl=ntl: call(
