@@ -134,13 +134,15 @@ __global__ __launch_bounds__(kBlock) void mix_vec_kernel(float* out, Fanin f, lo
 // Vector mix + fused compression epilogue (count reduction per block). Tiles of kBlock * U
 // float4 per block like mix_vec_kernel: U float4 of every stream per lane in flight together
 // (U = 4 while (N + 1) * U <= 40 registers' worth of float4, as auto_vec), nontemporal loads.
-template <int N>
+// The epilogue's form (KIND, compress_sel) is a template parameter.
+template <int N, int KIND>
 __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fanin f,
                                                                    long long nvec,
                                                                    CompressParams cp) {
   constexpr int U = (N + 1) * 4 <= 40 ? 4 : ((N + 1) * 2 <= 40 ? 2 : 1);
   constexpr long long kTile = (long long)kBlock * U;
   const Sc1Out o = sc1_out(out, nvec * 16);
+  const float thr = (float)cp.thr, rep = (float)cp.rep;
   unsigned kept = 0;
   for (long long base = (long long)blockIdx.x * kTile + threadIdx.x; base < nvec;
        base += (long long)gridDim.x * kTile) {
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void mix_vec_compress_kernel(float* out, Fa
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const long long e = e0 + c;
-          if (e >= cp.cbegin && e < cp.cend) w[c] = compress_one(w[c], r[c], cp, kept);
+          if (e >= cp.cbegin && e < cp.cend) w[c] = compress_sel<KIND>(w[c], r[c], thr, rep, kept);
         }
       }
       st16_sc1(o, i, w);
@@ -328,12 +330,12 @@ static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, 
   }
 }
 
-static void launch_vec_compress(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
-                                const CompressParams& cp) {
-  const unsigned grid = grid_for((nvec + kBlock - 1) / kBlock);
+template <int KIND>
+static void launch_vec_compress_k(int n, unsigned grid, hipStream_t st, float* out, const Fanin& f,
+                                  long long nvec, const CompressParams& cp) {
 #define CFA_CASE(K) \
   case K:           \
-    mix_vec_compress_kernel<K><<<grid, kBlock, 0, st>>>(out, f, nvec, cp); \
+    mix_vec_compress_kernel<K, KIND><<<grid, kBlock, 0, st>>>(out, f, nvec, cp); \
     break;
   switch (n) {
     CFA_CASE(0) CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6)
@@ -342,6 +344,16 @@ static void launch_vec_compress(int n, hipStream_t st, float* out, const Fanin& 
     default: break;
   }
 #undef CFA_CASE
+}
+
+static void launch_vec_compress(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
+                                const CompressParams& cp) {
+  const unsigned grid = grid_for((nvec + kBlock - 1) / kBlock);
+  switch (compress_kind(cp.mode)) {
+    case 1: launch_vec_compress_k<1>(n, grid, st, out, f, nvec, cp); break;
+    case 2: launch_vec_compress_k<2>(n, grid, st, out, f, nvec, cp); break;
+    default: launch_vec_compress_k<0>(n, grid, st, out, f, nvec, cp); break;
+  }
 }
 
 // One pass of at most CFA_MAX_FANIN neighbours. Splits the bucket into a scalar head (until

@@ -1063,7 +1063,7 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_fold64_di
 #define CFA_F(U, S) \
   if (u == U && sp == S) { fold64_x_kernel<4, U, S><<<grid, kBlock, 0, st>>>(out, f, nvec2); return check_launch("fold64_x"); }
   CFA_F(1, 0) CFA_F(1, 1) CFA_F(1, 2) CFA_F(1, 3) CFA_F(2, 0) CFA_F(2, 1) CFA_F(2, 2) CFA_F(2, 3)
-  CFA_F(4, 1) CFA_F(4, 2)
+  CFA_F(4, 1) CFA_F(4, 2) CFA_F(1, 3) CFA_F(4, 3)
 #undef CFA_F
   return fail(CFA_E_INVALID, "fold64 variant not instantiated");
 }
@@ -1092,7 +1092,7 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mewma64(
 #define CFA_M(U, S, L) \
   if (u == U && sp == S && ntl == L) { mewma64_x_kernel<2, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec2); return check_launch("mewma64_x"); }
   CFA_M(1, 1, 1) CFA_M(1, 2, 1) CFA_M(1, 0, 0) CFA_M(2, 1, 1) CFA_M(2, 2, 1) CFA_M(2, 0, 0) CFA_M(1, 3, 1)
-  CFA_M(2, 3, 1) CFA_M(1, 3, 0) CFA_M(2, 3, 0)
+  CFA_M(2, 3, 1) CFA_M(1, 3, 0) CFA_M(2, 3, 0) CFA_M(4, 3, 1) CFA_M(4, 1, 1) CFA_M(4, 2, 1)
 #undef CFA_M
   return fail(CFA_E_INVALID, "mewma64 variant not instantiated");
 }

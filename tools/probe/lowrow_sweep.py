@@ -104,7 +104,8 @@ def main():
         ref.copy_(out)
         variants = [("production (2 WG/CU, U=2, sc1 buffer store, full tiles)", prod, (2, 2))]
         for bpc, u, sp in [(1, 2, 2), (2, 2, 2), (1, 2, 1), (2, 2, 1), (2, 1, 1), (4, 1, 1), (2, 2, 3),
-                           (1, 4, 2), (2, 1, 2), (4, 1, 2)]:
+                           (1, 4, 2), (2, 1, 2), (4, 1, 2), (1, 1, 3), (1, 4, 3), (2, 4, 3), (4, 4, 3), (1, 2, 3),
+                           (4, 2, 3)]:
             fn = (lambda bpc=bpc, u=u, sp=sp: call("cfa_experimental_fold64_div", vp(out.data_ptr()), vp(loc.data_ptr()),
                                                    tb, ad, dd, ctypes.c_size_t(P), u, sp, bpc, vp(sh)))
             out.zero_()
@@ -136,7 +137,9 @@ def main():
         variants = [("production (1 WG/CU, U=1, nt loads/stores)", prod, (1, 1))]
         for bpc, u, sp, ntl in [(1, 2, 1, 1), (1, 2, 2, 1), (2, 1, 1, 1), (2, 2, 1, 1), (1, 1, 2, 1),
                                 (2, 1, 2, 1), (1, 2, 0, 0), (2, 1, 0, 0), (1, 1, 3, 1), (4, 1, 1, 1),
-                                (2, 1, 3, 1), (2, 2, 3, 1), (1, 2, 3, 1), (1, 1, 3, 0), (2, 1, 3, 0)]:
+                                (2, 1, 3, 1), (2, 2, 3, 1), (1, 2, 3, 1), (1, 1, 3, 0), (2, 1, 3, 0),
+                                (4, 4, 3, 1), (2, 4, 3, 1), (1, 4, 3, 1), (4, 2, 3, 1), (1, 4, 1, 1), (2, 4, 1, 1),
+                                (1, 4, 2, 1)]:
             fn = (lambda bpc=bpc, u=u, sp=sp, ntl=ntl: call(
                 "cfa_experimental_mewma64", vp(W.data_ptr()), st, gt, ctypes.c_double(rho), ctypes.c_double(lr1),
                 ctypes.c_double(lr2), ctypes.c_size_t(split), 1, ctypes.c_size_t(P), u, sp, ntl, bpc, vp(sh)))
