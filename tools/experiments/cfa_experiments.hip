@@ -1004,6 +1004,55 @@ __global__ __launch_bounds__(kBlock) void mewma64_x_kernel(XMewma a, long long n
   }
 }
 
+// Stream-major form of mewma64_x_kernel: every stream's U vectors are loaded back to back (as
+// rw_kernel does), and stored the same way, instead of one vector of each stream in turn.
+template <int N, int U, int SP, bool NTL>
+__global__ __launch_bounds__(kBlock) void mewma64_sm_kernel(XMewma a, long long nvec2) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec2 / kTile;
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (unsigned)(nvec2 * 16), 0x00020000);
+  __amdgpu_buffer_rsrc_t sr[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) sr[j] = __builtin_amdgcn_make_buffer_rsrc((void*)a.s[j], 0, (unsigned)(nvec2 * 16), 0x00020000);
+  xd2* W2 = reinterpret_cast<xd2*>(a.W);
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    xd2 Wv[U], g[U][N], s[U][N];
+#pragma unroll
+    for (int u = 0; u < U; ++u) Wv[u] = x_load<NTL>(reinterpret_cast<const xd2*>(a.W), base + (long long)u * kBlock);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) g[u][j] = x_load<true>(reinterpret_cast<const xd2*>(a.g[j]), base + (long long)u * kBlock);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[u][j] = x_load<NTL>(reinterpret_cast<const xd2*>(a.s[j]), base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) x_mewma<N>(Wv[u], g[u], s[u], 2 * (base + (long long)u * kBlock), a);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) x_store<xd2, SP>(reinterpret_cast<xd2*>(a.s[j]), sr[j], base + (long long)u * kBlock, s[u][j]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) x_store<xd2, SP>(W2, wr, base + (long long)u * kBlock, Wv[u]);
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec2; i += kBlock) {
+      xd2 Wv = W2[i], g[N], s[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        g[j] = reinterpret_cast<const xd2*>(a.g[j])[i];
+        s[j] = reinterpret_cast<const xd2*>(a.s[j])[i];
+      }
+      x_mewma<N>(Wv, g, s, 2 * i, a);
+#pragma unroll
+      for (int j = 0; j < N; ++j) reinterpret_cast<xd2*>(a.s[j])[i] = s[j];
+      W2[i] = Wv;
+    }
+  }
+}
+
 template <int U, int SP, bool NTL>
 __global__ __launch_bounds__(kBlock) void compress_full_kernel(float* y, const float* ref, long long nvec,
                                                               CompressParams cp) {
@@ -1094,6 +1143,11 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mewma64(
   CFA_M(1, 1, 1) CFA_M(1, 2, 1) CFA_M(1, 0, 0) CFA_M(2, 1, 1) CFA_M(2, 2, 1) CFA_M(2, 0, 0) CFA_M(1, 3, 1)
   CFA_M(2, 3, 1) CFA_M(1, 3, 0) CFA_M(2, 3, 0) CFA_M(4, 3, 1) CFA_M(4, 1, 1) CFA_M(4, 2, 1)
 #undef CFA_M
+  // sp + 10: the stream-major load / store order (mewma64_sm_kernel)
+#define CFA_SM(U, S, L) \
+  if (u == U && sp == S + 10 && ntl == L) { mewma64_sm_kernel<2, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec2); return check_launch("mewma64_sm"); }
+  CFA_SM(1, 1, 1) CFA_SM(2, 1, 1) CFA_SM(4, 1, 1) CFA_SM(4, 3, 1) CFA_SM(2, 3, 1) CFA_SM(4, 2, 1)
+#undef CFA_SM
   return fail(CFA_E_INVALID, "mewma64 variant not instantiated");
 }
 

@@ -139,7 +139,10 @@ def main():
                                 (2, 1, 2, 1), (1, 2, 0, 0), (2, 1, 0, 0), (1, 1, 3, 1), (4, 1, 1, 1),
                                 (2, 1, 3, 1), (2, 2, 3, 1), (1, 2, 3, 1), (1, 1, 3, 0), (2, 1, 3, 0),
                                 (4, 4, 3, 1), (2, 4, 3, 1), (1, 4, 3, 1), (4, 2, 3, 1), (1, 4, 1, 1), (2, 4, 1, 1),
-                                (1, 4, 2, 1)]:
+                                (1, 4, 2, 1),
+                                # sp + 10: stream-major load / store order (mewma64_sm_kernel)
+                                (1, 1, 11, 1), (1, 2, 11, 1), (1, 4, 11, 1), (1, 4, 13, 1), (2, 4, 13, 1),
+                                (4, 4, 13, 1), (2, 2, 13, 1), (1, 4, 12, 1), (2, 4, 11, 1)]:
             fn = (lambda bpc=bpc, u=u, sp=sp, ntl=ntl: call(
                 "cfa_experimental_mewma64", vp(W.data_ptr()), st, gt, ctypes.c_double(rho), ctypes.c_double(lr1),
                 ctypes.c_double(lr2), ctypes.c_size_t(split), 1, ctypes.c_size_t(P), u, sp, ntl, bpc, vp(sh)))
