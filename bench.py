@@ -302,8 +302,8 @@ def child_env(base: dict, t0: float, status_file: str) -> dict:
 def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python: str = None) -> int:
     """Run the N ranks as a child ``torch.distributed.run`` (never an exec: the parent has not
     touched the GPU, and exits with the child's status), relay rank 0's JSON line to stdout and
-    every other line of the child's stdout to stderr, and end the child's process group if it
-    outlives the total budget by ``grace`` seconds. Returns the run's exit status: rank 0's own
+    every other line of the child's stdout to stderr, and end the launcher (and with it the ranks)
+    if it outlives the total budget by ``grace`` seconds or this process is signalled. Returns the run's exit status: rank 0's own
     (status file) when it left one, else the launcher's."""
     import signal
     import subprocess
@@ -315,24 +315,38 @@ def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python
     os.unlink(status_file)  # created by the first rank that records a status
     cmd = child_command(argv, n, free_port(), python)
     print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    # the launcher stays in this process's group, so an outer time limit that signals the group
+    # (coreutils timeout does) reaches every rank too
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file),
-                            start_new_session=True, text=True, bufsize=1)
+                            text=True, bufsize=1)
     killed = threading.Event()
+
+    def end_child():
+        """SIGTERM to the launcher (torch.distributed.run ends its ranks on it), SIGKILL after 15 s."""
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            try:
+                proc.send_signal(sig)
+            except ProcessLookupError:
+                return
+            try:
+                proc.wait(timeout=15)
+                return
+            except subprocess.TimeoutExpired:
+                continue
 
     def kill_group():
         killed.set()
         print(f"[bench] FATAL: the ranks outlived the {total_seconds:.0f} s budget by {grace:.0f} s; "
               "ending them", file=sys.stderr, flush=True)
-        for sig in (signal.SIGTERM, signal.SIGKILL):
-            try:
-                os.killpg(proc.pid, sig)
-            except ProcessLookupError:
-                return
-            try:
-                proc.wait(timeout=10)
-                return
-            except subprocess.TimeoutExpired:
-                continue
+        end_child()
+
+    def on_signal(signum, frame):
+        print(f"[bench] signal {signum}: ending the ranks", file=sys.stderr, flush=True)
+        end_child()
+        os._exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, on_signal)
 
     timer = None
     if total_seconds > 0:

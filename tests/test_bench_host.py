@@ -230,3 +230,36 @@ def test_record_status_first_writer_wins(tmp_path, monkeypatch):
     bench.record_status(5)
     bench.record_status(0)
     assert path.read_text() == "5"
+
+
+def test_self_launch_forwards_a_termination_to_the_ranks(tmp_path):
+    """An outer time limit that signals the parent ends the launcher (and its ranks) as well; the
+    launcher is not detached into a session of its own."""
+    import signal
+    import subprocess
+    import time as _t
+    fake = tmp_path / "fakepy"
+    fake.write_text(FAKE_TORCHRUN)
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    pidfile = tmp_path / "child.pid"
+    code = ("import os, sys; sys.path.insert(0, %r); import bench, subprocess\n"
+            "orig = subprocess.Popen\n"
+            "def rec(*a, **k):\n"
+            "    p = orig(*a, **k); open(%r, 'w').write(str(p.pid)); return p\n"
+            "subprocess.Popen = rec\n"
+            "sys.exit(bench.self_launch(['--gpus', '2'], 2, 600, python=%r))" % (ROOT, str(pidfile), str(fake)))
+    parent = subprocess.Popen([sys.executable, "-c", code], env=dict(os.environ, FAKE_MODE="hang"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    for _ in range(100):
+        if pidfile.exists() and pidfile.read_text():
+            break
+        _t.sleep(0.1)
+    child = int(pidfile.read_text())
+    assert os.getpgid(child) == os.getpgid(parent.pid)  # same process group as the parent
+    _t.sleep(0.5)
+    parent.send_signal(signal.SIGTERM)
+    out, err = parent.communicate(timeout=60)
+    assert parent.returncode == 128 + signal.SIGTERM and "ending the ranks" in err
+    _t.sleep(0.2)
+    with pytest.raises(ProcessLookupError):
+        os.kill(child, 0)
