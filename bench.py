@@ -915,6 +915,11 @@ def main():
                 "launches_timed": launches_timed,
                 "bytes_per_launch": per_launch_bytes,
                 "timing": "HIP events around each step's back-to-back interior mixes / launches",
+                # the whole job against the aggregate HBM peak of its GPUs (north_star: GB/s at
+                # 1/2/4/8 GPUs "as absolute numbers and as fraction of the HBM roofline"); at N > 1
+                # this includes the exchange
+                "job_peak": HBM_PEAK_GBS * world,
+                "job_frac": round(value / (HBM_PEAK_GBS * world), 4),
                 "cache_reuse": reuse,
                 "traffic": load_traffic(
                     args.traffic_json or os.path.join(ROOT, "profiles", "r01_window_pmc_traffic.json"

@@ -30,6 +30,7 @@ def test_bench_line_contract():
     rl = d["roofline"]
     assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
     assert 0 < rl["frac"] < 1 and abs(rl["frac"] - rl["achieved"] / rl["peak"]) < 1e-3
+    assert rl["job_peak"] == 8000.0 and abs(rl["job_frac"] - d["value"] / 8000.0) < 1e-3
     assert "traffic" in rl
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]
@@ -71,6 +72,7 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     assert c["transport"] == "torch-gloo" and c["comparable"] is False
     assert set(c["halo_route"]) >= {"relay", "stages", "critical_MB", "autotune"}
     assert set(c["budget"]) >= {"total_s", "headline_s", "left_s", "skipped"}
+    assert d["roofline"]["job_peak"] == 16000.0 and abs(d["roofline"]["job_frac"] - d["value"] / 16000.0) < 1e-3
     # 1M-element rows: a 9-row window fits the Infinity Cache, so the scattered rate is there too
     assert c["cache_reuse"] is True and isinstance(d["value_scattered"], float) and c["rows_note"]
     p = d["partitions"]["params"]
