@@ -41,8 +41,9 @@ is always measured; the extra legs, the CPU baselines, the PMC passes and the e2
 only if the budget left covers their estimate, otherwise they are listed as ``skipped: budget``.
 
 Exit status: 0 = the line is complete; 3 = the transport the headline needs (RCCL) could not be
-opened on every rank (the line is printed with the ``params`` partition, which exchanges nothing,
-as ``value`` and ``config.headline_fallback`` saying why); 5 = the line is printed but an extra
+opened on every rank, or the exchanging headline raised on every rank (the line is printed with
+the ``params`` partition, which exchanges nothing, as ``value`` and ``config.headline_fallback``
+saying why); 5 = the line is printed but an extra
 leg failed, ran out of its budget or lost a peer (named in ``partitions``); 124 = the watchdog
 ended a run stuck in its headline (no line). Self-launched, the parent returns the same status.
 """
@@ -825,11 +826,35 @@ def main():
             xshard.mix_order = None
         return xel, xdur
 
+    def measure_headline(partition):
+        watchdog.enter(f"build {partition} shard")
+        xshard, xinfo, xtune = build_tuned(partition)
+        watchdog.enter("timed rounds")
+        return (xshard, xinfo, xtune) + run_leg(args, xshard, world, args.steps, args.warmup)
+
     t_head0 = time.time()
-    watchdog.enter(f"build {headline} shard")
-    shard, info, autotune = build_tuned(headline)
-    watchdog.enter("timed rounds")
-    elapsed, durations, launches_per_step = run_leg(args, shard, world, args.steps, args.warmup)
+    if world == 1:
+        shard, info, autotune, elapsed, durations, launches_per_step = measure_headline(headline)
+    else:
+        # an exchanging headline that fails on every rank alike (an RCCL error in the first rounds
+        # of a node this build never ran on) still gives a line: the params partition, which
+        # exchanges nothing, then measures the headline and the run exits 3, as for a transport
+        # that cannot open. (A failure on some ranks only leaves the others inside a collective;
+        # the watchdog ends that run.)
+        err = None
+        try:
+            res = measure_headline(headline)
+        except Exception as exc:
+            err = f"{type(exc).__name__}: {exc}"
+            print(f"[bench rank {rank}] {headline} headline failed: {err}", file=sys.stderr, flush=True)
+        if not agree_all(err is None):
+            if headline == "params":
+                raise RuntimeError(f"the params headline failed ({err or 'on another rank'})")
+            headline_fallback = {"wanted": headline, "measured": "params",
+                                 "error": err or "the headline failed on another rank"}
+            headline, headline_exchanges = "params", False
+            res = measure_headline("params")
+        shard, info, autotune, elapsed, durations, launches_per_step = res
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
     interior = shard.interior_order()
@@ -974,19 +999,21 @@ def main():
 
         def report_early(name, why):
             """Rank 0: print the line once, with the legs measured so far and ``name`` marked with
-            ``why`` (the headline is complete). Returns the exit status, 5. The other ranks give rank
-            0 time to print first (torch.distributed.run ends every rank once one has exited)."""
+            ``why`` (the headline is complete). Returns the exit status: 5, or 3 after a headline
+            fallback. The other ranks give rank 0 time to print first (torch.distributed.run ends
+            every rank once one has exited)."""
+            code = EXIT_TRANSPORT if headline_fallback else EXIT_LEG
             with report_lock:
                 if rank == 0 and not report_early.done:
                     out = json.loads(json.dumps(result))
                     out["partitions"][name] = {"error": why, "note": notes[name]}
-                    out["exit_status"] = EXIT_LEG
+                    out["exit_status"] = code
                     print(json.dumps(out), flush=True)
-                    record_status(EXIT_LEG)
+                    record_status(code)
                     report_early.done = True
             if rank != 0:
                 wait_for_status(15.0)
-            return EXIT_LEG
+            return code
         report_early.done = False
 
         def leg_expired(name, seconds):

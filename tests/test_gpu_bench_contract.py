@@ -92,3 +92,15 @@ def test_self_launched_n2_rccl_refused_falls_back_and_exits_3():
     assert fb["wanted"] == "devices" and fb["measured"] == "params" and "rccl" in fb["error"]
     assert d["config"]["partition"] == "params" and d["value"] > 0
     assert "error" in d["partitions"]["devices"]
+
+
+def test_self_launched_headline_failing_on_every_rank_falls_back_and_exits_3():
+    """An exchanging headline that raises on every rank (here a hybrid partition whose device groups
+    do not divide the world) still yields the line: the params partition measured as the headline,
+    the error in config.headline_fallback, status 3."""
+    r, d = _self_launched(["--transport", "torch", "--partition", "hybrid", "--device-groups", "3",
+                           "--no-extra-legs"])
+    assert r.returncode == 3 and d["exit_status"] == 3
+    fb = d["config"]["headline_fallback"]
+    assert fb["wanted"] == "hybrid" and fb["measured"] == "params" and "dev_groups" in fb["error"]
+    assert d["config"]["partition"] == "params" and d["value"] > 0
