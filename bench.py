@@ -1005,7 +1005,16 @@ def main():
             code = EXIT_TRANSPORT if headline_fallback else EXIT_LEG
             with report_lock:
                 if rank == 0 and not report_early.done:
-                    out = json.loads(json.dumps(result))
+                    out = None
+                    for _ in range(50):  # the main thread may be adding a leg right now
+                        try:
+                            out = json.loads(json.dumps(result))
+                            break
+                        except RuntimeError:
+                            time.sleep(0.01)
+                    if out is None:
+                        out = {k: v for k, v in result.items() if k != "partitions"}
+                        out["partitions"] = {}
                     out["partitions"][name] = {"error": why, "note": notes[name]}
                     out["exit_status"] = code
                     print(json.dumps(out), flush=True)
