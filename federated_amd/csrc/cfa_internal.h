@@ -173,62 +173,33 @@ struct Fanin {
   const float* src[CFA_MAX_FANIN + 1];  // [0] = local (w0), [1..N] = neighbours
   float c[CFA_MAX_FANIN + 1];           // SEQ: c[j] = alpha of src[j] (c[0] unused); LIN: coeff
   float d[CFA_MAX_FANIN + 1];           // SEQ_DIV: d[j] = divisor of step j (d[0] unused)
-  float r[CFA_MAX_FANIN + 1];           // SEQ_DIV: r[j] = RN(1 / d[j]) (fast_div)
-  int fast_div;                         // every d[j] in [2^-20, 2^20]: div_rn's fast path applies
+  double rd[CFA_MAX_FANIN + 1];         // SEQ_DIV: rd[j] = RN_64(1 / d[j]) (div4_rn)
 };
 
-// Correctly rounded a / b from rb = RN(1/b) (Markstein): q = RN(a * rb) is within 1 ulp of
-// a / b, the remainder r = a - b q is exact (one fma), and RN(q + r * rb) is the correctly
-// rounded quotient, i.e. exactly IEEE a / b. That holds when nothing under- or overflows, which
-// the range guard ensures (|a| in [2^-100, 2^100] and b in [2^-20, 2^20] make q, r and the
-// quotient normal); every other a (zeros, subnormals, huge, inf, NaN) takes the IEEE division.
-// Three instructions instead of the divide sequence (v_div_scale x2, v_rcp, v_div_fmas,
-// v_div_fixup, four fma); tested bit for bit against numpy over wide exponent ranges.
-__device__ __forceinline__ float div_rn(float a, float b, float rb, bool fast) {
-  const float aa = __builtin_fabsf(a);
-  if (fast && aa >= 0x1p-100f && aa <= 0x1p100f) {
-    const float q = a * rb;
-    const float r = __builtin_fmaf(-q, b, a);
-    return __builtin_fmaf(r, rb, q);
-  }
-  return a / b;
+// Correctly rounded fp32 a / b as ONE fp64 multiply: (float)((double)a * RN_64(1/b)) is exactly
+// IEEE a / b for every fp32 a and b, with no range guard. The exact quotient of two 24-bit
+// significands lies at least 2^-48 (relative) from every fp32 rounding midpoint, normal or
+// subnormal, while the two fp64 roundings (of 1/b and of the product) stay within 2^-52 of it;
+// fp64's exponent range holds every fp32 quotient (so fp32 overflow and underflow happen in the
+// final conversion, as in the IEEE division), and zeros, infinities and NaN propagate as they do
+// there (0 * inf = NaN for 0/0, x * 0 = 0 for x/inf). Two conversions and one v_mul_f64 per
+// element, branch-free; round 4 replaced Markstein's three fp32 operations plus a range test per
+// float4 with it (tools/probe/lowrow_sweep.py --only div, profiles/r04_div64_sweep.jsonl: 0.733 ->
+// 0.776 of peak at 25M, n = 8). Tested bit for bit against numpy over every binade
+// (tests/test_gpu_div.py; 10^8 random bit patterns on the CPU, tests/test_div64_rule.py).
+__device__ __forceinline__ float div_rd(float a, double rb) { return (float)((double)a * rb); }
+__device__ __forceinline__ f4 div4_rn(f4 a, double rb) {
+  f4 q;
+  q.x = div_rd(a.x, rb);
+  q.y = div_rd(a.y, rb);
+  q.z = div_rd(a.z, rb);
+  q.w = div_rd(a.w, rb);
+  return q;
 }
 
-// div_rn on the four lanes of a float4 with ONE range test for all four: the Markstein steps run
-// on every lane, and only when some |a| lies outside the guard (zeros, subnormals, huge values,
-// infinities) does the IEEE division redo the four lanes. max3/min3 of the magnitudes replace four
-// pairs of compares and four exec-mask branches. A NaN lane passes through either path as a NaN
-// (fmaxf/fminf skip it; Markstein on a NaN gives a NaN).
-__device__ __forceinline__ f4 div4_rn(f4 a, float b, float rb, bool fast) {
-  const float mx = fmaxf(fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)),
-                         fmaxf(__builtin_fabsf(a.z), __builtin_fabsf(a.w)));
-  const float mn = fminf(fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)),
-                         fminf(__builtin_fabsf(a.z), __builtin_fabsf(a.w)));
-  if (fast && mn >= 0x1p-100f && mx <= 0x1p100f) {
-    f4 q = a * rb;
-    f4 r;
-    r.x = __builtin_fmaf(-q.x, b, a.x);
-    r.y = __builtin_fmaf(-q.y, b, a.y);
-    r.z = __builtin_fmaf(-q.z, b, a.z);
-    r.w = __builtin_fmaf(-q.w, b, a.w);
-    q.x = __builtin_fmaf(r.x, rb, q.x);
-    q.y = __builtin_fmaf(r.y, rb, q.y);
-    q.z = __builtin_fmaf(r.z, rb, q.z);
-    q.w = __builtin_fmaf(r.w, rb, q.w);
-    return q;
-  }
-  return a / b;
-}
-
-// Host side: fills f.r / f.fast_div from f.d[0..n].
+// Host side: fills f.rd from f.d[0..n].
 inline void set_reciprocals(Fanin& f, int n) {
-  bool fast = true;
-  for (int k = 0; k <= n; ++k) {
-    const float d = f.d[k];
-    f.r[k] = 1.0f / d;
-    if (k >= 1 && !(d >= 0x1p-20f && d <= 0x1p20f)) fast = false;
-  }
-  f.fast_div = fast ? 1 : 0;
+  for (int k = 0; k <= n; ++k) f.rd[k] = 1.0 / (double)f.d[k];
 }
 
 template <bool NT>
@@ -261,7 +232,7 @@ __device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
     for (int j = 1; j <= N; ++j) {
       f4 t = v[j] - w;  // numpy: (x - w)
       t = f.c[j] * t;   //        u * (...)
-      t = div4_rn(t, f.d[j], f.r[j], f.fast_div);  // (...) / C, IEEE-correct fp32 division
+      t = div4_rn(t, f.rd[j]);  // (...) / C, IEEE-correct fp32 division
       w = w + t;
     }
     return w;

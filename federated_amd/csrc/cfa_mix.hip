@@ -294,17 +294,20 @@ static void launch_vec(int n, hipStream_t st, float* out, const Fanin& f, long l
 template <int RULE>
 static void launch_vec_chunk(int n, hipStream_t st, float* out, const Fanin& f, long long nvec,
                              const cfa_launch_t& t) {
-  // the divisor fold carries a guarded division per element and step: one float4 per lane
-  // keeps more tiles in flight per VGPR budget (tools/probe/div_sweep.py: 6.03 vs 5.69 TB/s)
   // library default (blocks_per_cu == kAutoBlocks): the mix's own shape, one workgroup per CU;
   // an explicit configuration (cfa_mix_seq_ex_f32, CFA_BLOCKS_PER_CU) keeps the round-1 auto vec
   // (the sequential rule only: the linear closed form measured 0.752 with it against 0.790 with
   // two workgroups x 4 float4 on the same buffers, profiles/r02_s3_kernel_rooflines_vec_same.jsonl)
-  const bool own = t.blocks_per_cu == kAutoBlocks && RULE == CFA_RULE_SEQUENTIAL;
+  // The divisor fold (fp64-reciprocal division since round 4) takes the mix's shape too, with the
+  // round-1 auto vec in the one-workgroup branch: at 25M, n = 8, one workgroup x four float4 ran
+  // 0.776 of peak against 0.749 at two workgroups x one float4 (the Markstein form's shape) and
+  // 0.760 at one x two (profiles/r04_div64_sweep.jsonl).
+  const bool own = t.blocks_per_cu == kAutoBlocks &&
+                   (RULE == CFA_RULE_SEQUENTIAL || RULE == CFA_RULE_SEQUENTIAL_DIV);
   int own_bpc = 1, own_vec = 1;
   if (own) mix_auto_shape(n, nvec, own_bpc, own_vec);
-  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane)
-                                   : (RULE == CFA_RULE_SEQUENTIAL_DIV ? 1 : (own ? own_vec : auto_vec(n)));
+  if (own && RULE == CFA_RULE_SEQUENTIAL_DIV && own_bpc == 1) own_vec = auto_vec(n);
+  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : (own ? own_vec : auto_vec(n));
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   cfa_launch_t shape = t;
   if (own) shape.blocks_per_cu = own_bpc;

@@ -114,9 +114,11 @@ struct F64Fanin {
   int fast_div;                          // every d[j] in [2^-20, 2^20]
 };
 
-// fp64 counterpart of div_rn (cfa_internal.h): Markstein's correction from RN(1/b) is the
-// correctly rounded quotient when nothing under- or overflows; |a| in [2^-900, 2^900] and b in
-// [2^-20, 2^20] guarantee that, everything else takes the IEEE division.
+// Correctly rounded fp64 a / b (Markstein): q = RN(a * rb) with rb = RN(1/b) is within 1 ulp,
+// the remainder a - b q is exact (one fma), and RN(q + r * rb) is the correctly rounded quotient
+// when nothing under- or overflows; |a| in [2^-900, 2^900] and b in [2^-20, 2^20] guarantee
+// that, everything else takes the IEEE division. (The fp32 fold's one-multiply form, div_rd in
+// cfa_internal.h, needs a format twice as wide; fp64 has none on the GPU.)
 __device__ __forceinline__ double ddiv_rn(double a, double b, double rb, bool fast) {
   const double aa = __builtin_fabs(a);
   if (fast && aa >= 0x1p-900 && aa <= 0x1p900) {

@@ -545,14 +545,21 @@ def test_special_values_follow_numpy(gpu, n):
     assert _same_bits_or_nan(o64.cpu().numpy(), r64)
 
 
+_RAND_DIVISORS = [float(v) for v in np.random.default_rng(4244).integers(0, 0x7F7FFFFF, 24, dtype=np.uint32)
+                  .view(np.float32)]
+
+
 @pytest.mark.parametrize("divisors", [[float(c) for c in range(1, 65)],
                                       [3.0, 7.0, 1e-7, 3e7, 0.1, 1023.0, 2.0 ** 20, 2.0 ** -20],
-                                      [float(c) for c in (97, 255, 4095, 65535, 1048575)]])
+                                      [float(c) for c in (97, 255, 4095, 65535, 1048575)],
+                                      [1e-40, 1.4e-45, -3.0, -0.1, 3.4028235e38, 1e-38, 0.0, -0.0, np.inf],
+                                      _RAND_DIVISORS])
 def test_mix_seq_div_quotient_exact_over_exponent_range(gpu, divisors):
-    """The fold's division (reciprocal + one fma correction inside a range guard, IEEE division
-    outside it) equals numpy's fp32 a / C bit for bit: with local = 0 and u = 1 the one-step fold
-    is 0 + x / C, for x spread over every binade from 2^-149 to 2^127 (zeros, subnormals, the
-    guard's edges, infinities and NaN included) and divisors inside and outside the fast range."""
+    """The fold's division (one fp64 multiply by RN_64(1/C), cfa_internal.h div_rd) equals numpy's
+    fp32 a / C bit for bit: with local = 0 and u = 1 the one-step fold is 0 + x / C, for x spread
+    over every binade from 2^-149 to 2^127 (zeros, subnormals, the old Markstein guard's edges,
+    infinities and NaN included) and divisors over every binade (subnormal, negative, the largest
+    finite, zero and infinity included, plus 24 random fp32 bit patterns)."""
     rng = np.random.default_rng(4242)
     P = 1 << 22
     mant = rng.integers(0, 1 << 23, P, dtype=np.uint32)
