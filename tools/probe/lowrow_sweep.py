@@ -191,7 +191,7 @@ def main():
         prod()
         torch.cuda.synchronize()
         ref.copy_(out)
-        variants = [("production (2 WG/CU, 1 float4, Markstein division, sc1 store)", prod, (2, 1))]
+        variants = [("production (own shape; Markstein division before fe0073c, fp64-reciprocal after)", prod, None)]
         for bpc, u, sp in [(2, 1, 3), (1, 2, 3), (2, 2, 3), (4, 1, 3), (1, 4, 3), (2, 1, 1), (1, 2, 2), (4, 2, 3)]:
             fn = (lambda bpc=bpc, u=u, sp=sp: call("cfa_experimental_div64", vp(out.data_ptr()), vp(loc.data_ptr()),
                                                    tb, af, df, ctypes.c_size_t(P), u, sp, bpc, vp(sh)))
