@@ -55,6 +55,24 @@ def test_mix_seq_bitexact_across_launch_shape_bands(gpu, n):
         assert np.array_equal(out.cpu().numpy(), ref), (n, P)
 
 
+@pytest.mark.parametrize("n", [2, 8, 12])
+def test_mix_seq_div_bitexact_across_launch_shape_bands(gpu, n):
+    """The divisor fold takes the mix's shape bands since round 4, with four float4 per lane (two
+    above nine neighbours) in the one-workgroup band from 8M elements: sizes on both sides of the
+    band edges, ragged tails, a divisor that is not a power of two, u != 1, in place at 8M+."""
+    rng = np.random.default_rng(320 + n)
+    for P in [524_293, 1_572_873, 3_145_741, 8_388_607, 8_388_613, 9_000_005]:
+        local = _rand(rng, 1, P)[0]
+        nbrs = _rand(rng, n, P)
+        w = local.copy()  # parameter_server_v2.py:159-161 with u = 0.99, C = 7 (fp32 numpy)
+        for x in nbrs:
+            w = w + np.float32(0.99) * (x - w) / np.float32(7.0)
+        inplace = P > 8_388_608
+        out = _dev(local) if inplace else torch.empty(P, dtype=torch.float32, device="cuda")
+        gpu.mix_seq_div(out, out if inplace else _dev(local), [_dev(x) for x in nbrs], [0.99] * n, [7.0] * n)
+        assert np.array_equal(out.cpu().numpy(), w), (n, P)
+
+
 def test_mix_seq_varied_alphas_and_inplace(gpu):
     rng = np.random.default_rng(7)
     P = 1_000_003
