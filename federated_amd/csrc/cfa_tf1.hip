@@ -30,46 +30,86 @@ struct Tf1Fanin {
 // pass (no epilogue), or the unrounded fp64 result (epilogue in fp64, no rounding).
 enum { kOutF32 = 0, kOutScratch64 = 1, kOutF64 = 2 };
 
+// One float4 of the TF1 chain: x = the N neighbour vectors, l = the local vector, w64 = the
+// previous pass's running fp64 w (FROM64), i = the vector's index. Epilogue, rounding and store.
 template <int N, bool FROM64, int OUT>
+__device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fanin& f, const f4 (&x)[N],
+                                        const f4& l, const double* w64, long long i, const CompressParams& cp,
+                                        int compress, unsigned& kept) {
+  double w[4];
+  constexpr int j0 = FROM64 ? 0 : 1;
+  if constexpr (FROM64) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = w64[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float d = x[0][c] - l[c];            // fp32 - fp32 (both operands fp32)
+      w[c] = (double)l[c] + f.a[0] * (double)d;  // np.float64 * fp32 -> fp64; fp32 + fp64 -> fp64
+    }
+  }
+#pragma unroll
+  for (int j = j0; j < N; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
+  if (OUT != kOutScratch64 && compress) {
+    const long long e0 = i * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
+  }
+  if constexpr (OUT == kOutF32) {
+    const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+    st16_sc1(o, i, y);
+  } else {  // fp64 out: plain stores (two sc1 halves per lane measured 17% slower)
+    double* od = reinterpret_cast<double*>(out) + 4 * i;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) od[c] = w[c];
+  }
+}
+
+// Full tiles of kBlock * U float4 per block (grid-stride over tiles, every load of a tile issued
+// before its first use, nontemporal loads), the partial last tile by the block that owns it with
+// per-vector guards: the headline mix's skeleton (round 4).
+template <int N, bool FROM64, int OUT, int U>
 __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin f, long long nvec,
                                                               CompressParams cp, int compress) {
+  constexpr long long kTile = (long long)kBlock * U;
   unsigned kept = 0;
   const Sc1Out o = sc1_out(out, nvec * 16);  // used by the fp32 output only
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < nvec;
-       i += (long long)gridDim.x * kBlock) {
-    f4 x[N];
+  const long long full = nvec / kTile;
+  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
+    const long long base = t * kTile + threadIdx.x;
+    f4 x[U][N], l[U];
 #pragma unroll
-    for (int k = 0; k < N; ++k) x[k] = ld4<true>(f.src[k], i);
-    const f4 l = ld4<true>(f.local, i);
-    double w[4];
-    constexpr int j0 = FROM64 ? 0 : 1;
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) l[u] = ld4<true>(f.local, base + (long long)u * kBlock);
+    double w64[U][4];
     if constexpr (FROM64) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) w[c] = f.w64[4 * i + c];
-    } else {
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float d = x[0][c] - l[c];         // fp32 - fp32 (both operands fp32)
-        w[c] = (double)l[c] + f.a[0] * (double)d;  // np.float64 * fp32 -> fp64; fp32 + fp64 -> fp64
+        for (int c = 0; c < 4; ++c) w64[u][c] = f.w64[4 * (base + (long long)u * kBlock) + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      tf1_vec<N, FROM64, OUT>(out, o, f, x[u], l[u], w64[u], base + (long long)u * kBlock, cp, compress, kept);
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
+      f4 x[N];
+#pragma unroll
+      for (int k = 0; k < N; ++k) x[k] = ld4<true>(f.src[k], i);
+      const f4 l = ld4<true>(f.local, i);
+      double w64[4];
+      if constexpr (FROM64) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w64[c] = f.w64[4 * i + c];
       }
-    }
-#pragma unroll
-    for (int j = j0; j < N; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
-    if (OUT != kOutScratch64 && compress) {
-      const long long e0 = i * 4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
-    }
-    if constexpr (OUT == kOutF32) {
-      const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
-      st16_sc1(o, i, y);
-    } else {  // fp64 out: plain stores (two sc1 halves per lane measured 17% slower)
-      double* od = reinterpret_cast<double*>(out) + 4 * i;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) od[c] = w[c];
+      tf1_vec<N, FROM64, OUT>(out, o, f, x, l, w64, i, cp, compress, kept);
     }
   }
   if (OUT != kOutScratch64 && compress) block_add_count(kept, cp.kept);
@@ -360,12 +400,12 @@ static void launch_mewma_f64_vec(int m, unsigned grid, hipStream_t st, const Mew
      ...);
 }
 
-template <bool FROM64, int OUT>
-static void launch_tf1_vec(int n, unsigned grid, hipStream_t st, void* out, const Tf1Fanin& f,
-                           long long nvec, const CompressParams& cp, int compress) {
+template <bool FROM64, int OUT, int U>
+static void launch_tf1_vec_u(int n, unsigned grid, hipStream_t st, void* out, const Tf1Fanin& f,
+                             long long nvec, const CompressParams& cp, int compress) {
 #define CFA_CASE(K) \
   case K:           \
-    mix_tf1_vec_kernel<K, FROM64, OUT><<<grid, kBlock, 0, st>>>(out, f, nvec, cp, compress); \
+    mix_tf1_vec_kernel<K, FROM64, OUT, U><<<grid, kBlock, 0, st>>>(out, f, nvec, cp, compress); \
     break;
   switch (n) {
     CFA_CASE(1) CFA_CASE(2) CFA_CASE(3) CFA_CASE(4) CFA_CASE(5) CFA_CASE(6) CFA_CASE(7)
@@ -374,6 +414,24 @@ static void launch_tf1_vec(int n, unsigned grid, hipStream_t st, void* out, cons
     default: break;
   }
 #undef CFA_CASE
+}
+
+// Launch shape of the TF1 vector kernel: the library default or an explicit CFA_VEC_PER_LANE /
+// CFA_BLOCKS_PER_CU. Default (round 4, tools/kernel_rooflines.py A/B, two alternated rounds on one
+// box, profiles/r04_tf1_ab_rooflines.jsonl): fp32 out two float4 per lane at two workgroups per CU
+// (0.782 / 0.783 of peak at 25M, n = 8, against 0.757 / 0.755 for the one-vector grid-stride
+// kernel before; one float4: 0.743, four: 0.757); fp64 out four float4 at one workgroup per CU
+// (0.751 / 0.757 against 0.754 / 0.754 before; two float4: 0.668, one: 0.746).
+template <bool FROM64, int OUT>
+static void launch_tf1_vec(int n, hipStream_t st, void* out, const Tf1Fanin& f, long long nvec,
+                           const CompressParams& cp, int compress) {
+  const cfa_launch_t& t = tune();
+  const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : (OUT == kOutF32 ? 2 : 4);
+  const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
+  const unsigned grid = OUT == kOutF64 ? grid_for_own(tiles, 1) : grid_for(tiles);
+  if (U == 4) launch_tf1_vec_u<FROM64, OUT, 4>(n, grid, st, out, f, nvec, cp, compress);
+  else if (U == 2) launch_tf1_vec_u<FROM64, OUT, 2>(n, grid, st, out, f, nvec, cp, compress);
+  else launch_tf1_vec_u<FROM64, OUT, 1>(n, grid, st, out, f, nvec, cp, compress);
 }
 
 // One TF1 pass of 1..CFA_MAX_FANIN neighbours over [0, P): `head` scalar elements, a float4
@@ -405,20 +463,18 @@ static int tf1_pass(void* out, int out_mode, const float* local, const double* w
     const Tf1Fanin f = fanin_at(head);
     // the fp64-output (wide) form runs one workgroup per CU: 0.749 against 0.729 of peak on the
     // same buffers (tools/kernel_rooflines.py --bpc-variants 2,1); the fp32 outputs keep two
-    const long long vt = ((long long)nvec + kBlock - 1) / kBlock;
-    const unsigned grid = out_mode == kOutF64 ? grid_for_own(vt, 1) : grid_for(vt);
     const CompressParams c = shifted(head);
     void* o = out_at(head);
     const long long nv = (long long)nvec;
     if (out_mode == kOutF32) {
-      if (w64) launch_tf1_vec<true, kOutF32>(m, grid, st, o, f, nv, c, compress);
-      else launch_tf1_vec<false, kOutF32>(m, grid, st, o, f, nv, c, compress);
+      if (w64) launch_tf1_vec<true, kOutF32>(m, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutF32>(m, st, o, f, nv, c, compress);
     } else if (out_mode == kOutScratch64) {
-      if (w64) launch_tf1_vec<true, kOutScratch64>(m, grid, st, o, f, nv, c, compress);
-      else launch_tf1_vec<false, kOutScratch64>(m, grid, st, o, f, nv, c, compress);
+      if (w64) launch_tf1_vec<true, kOutScratch64>(m, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutScratch64>(m, st, o, f, nv, c, compress);
     } else {
-      if (w64) launch_tf1_vec<true, kOutF64>(m, grid, st, o, f, nv, c, compress);
-      else launch_tf1_vec<false, kOutF64>(m, grid, st, o, f, nv, c, compress);
+      if (w64) launch_tf1_vec<true, kOutF64>(m, st, o, f, nv, c, compress);
+      else launch_tf1_vec<false, kOutF64>(m, st, o, f, nv, c, compress);
     }
     if (int rc = check_launch("mix_tf1_vec")) return rc;
   }
