@@ -38,7 +38,7 @@ def test_mix_seq_bitexact(gpu, n):
         assert np.array_equal(out.cpu().numpy(), ref), (n, P)
 
 
-@pytest.mark.parametrize("n", [2, 4, 8, 12, 16])
+@pytest.mark.parametrize("n", [2, 4, 8, 12, 16, 20])
 def test_mix_seq_bitexact_across_launch_shape_bands(gpu, n):
     """The default launch shape depends on the bucket size (cfa_internal.h mix_auto_shape): one
     workgroup per CU from 8M elements, four below (1 float4 per lane from 512K, 4 from 1.5M, 2 for
@@ -55,7 +55,7 @@ def test_mix_seq_bitexact_across_launch_shape_bands(gpu, n):
         assert np.array_equal(out.cpu().numpy(), ref), (n, P)
 
 
-@pytest.mark.parametrize("n", [2, 8, 12])
+@pytest.mark.parametrize("n", [2, 8, 12, 20])
 def test_mix_seq_div_bitexact_across_launch_shape_bands(gpu, n):
     """The divisor fold takes the mix's shape bands since round 4, with four float4 per lane (two
     above nine neighbours) in the one-workgroup band from 8M elements: sizes on both sides of the
