@@ -11,8 +11,8 @@ reference's per-layer arrays to and from that flat form.
 from __future__ import annotations
 
 import contextlib
-
 import ctypes
+import functools
 from typing import Iterable, Optional, Sequence
 
 import numpy as np
@@ -48,6 +48,32 @@ def _check_bucket(t: torch.Tensor, name: str, P: Optional[int] = None, dtype=tor
     if P is not None and n != P:
         raise ValueError(f"{name} has {n} elements, expected {P}")
     return n
+
+
+def _foreign(objs, index: int):
+    """The first CUDA tensor or stream in ``objs`` (tensors, streams, and lists / tuples of them)
+    that is not on GPU ``index``, else None."""
+    for a in objs:
+        for t in (a if isinstance(a, (list, tuple)) else (a,)):
+            if isinstance(t, torch.Tensor):
+                if t.is_cuda and t.device.index != index:
+                    return t.device
+            elif isinstance(t, torch.cuda.Stream) and t.device.index != index:
+                return t.device
+    return None
+
+
+def _same_device(fn):
+    """Engine method guard: every CUDA tensor and stream argument must be on the engine's GPU. A
+    kernel enqueued on this GPU's stream with another GPU's pointers would fault (no peer mapping)
+    or, with one, silently run over xGMI; both are caller errors, refused before any launch."""
+    @functools.wraps(fn)
+    def checked(self, *args, **kwargs):
+        dev = _foreign(list(args) + list(kwargs.values()), self.device.index)
+        if dev is not None:
+            raise ValueError(f"{fn.__name__}: argument on {dev}, but this engine runs on {self.device}")
+        return fn(self, *args, **kwargs)
+    return checked
 
 
 def _check_2d(t: torch.Tensor, name: str):
@@ -581,6 +607,12 @@ class Engine:
 
 
 _engines: dict = {}
+
+
+for _name, _fn in list(vars(Engine).items()):
+    if (callable(_fn) and not isinstance(_fn, (staticmethod, classmethod)) and not _name.startswith("_")
+            and _name not in ("empty", "counter", "stream_handle", "grad_workspace", "grad_splits")):
+        setattr(Engine, _name, _same_device(_fn))
 
 
 def get_engine(device=None) -> Engine:

@@ -476,6 +476,20 @@ def test_error_paths(gpu):
         gpu.mix_seq(x, torch.zeros(16, device="cuda", dtype=torch.float64), [], [])
 
 
+def test_arguments_on_another_gpu_are_refused(gpu, monkeypatch):
+    """An engine bound to one GPU refuses tensors and streams of another before any launch (on a
+    one-GPU box: the engine is told it runs on cuda:1, the arguments stay on cuda:0)."""
+    monkeypatch.setattr(gpu, "device", torch.device("cuda", 1))
+    x, y = torch.zeros(16, device="cuda:0"), torch.zeros(16, device="cuda:0")
+    for call in (lambda: gpu.mix_seq(x, y, [y], [0.5]),
+                 lambda: gpu.prepare_mix_seq(x, y, [y], [0.5]),
+                 lambda: gpu.mix_seq_div(x, y, [y], [1.0], [2.0]),
+                 lambda: gpu.mewma(x, [y], [y], 0.99, 0.1, 0.1, 16, False, True),
+                 lambda: gpu.compress(x, None, 1, torch.zeros(1, dtype=torch.int64, device="cuda:0"))):
+        with pytest.raises(ValueError, match="this engine runs on cuda:1"):
+            call()
+
+
 @pytest.mark.parametrize("n", [1, 3, 7, 20])
 def test_mix_seq_div_bitexact(gpu, n):
     """FedAvg form p <- p + u*(x - p)/C (parameter_server_v2.py:159-161), fp32 numpy rounding."""
