@@ -15,7 +15,10 @@
  *     form is cfa_mix_tf1_ex_f32). The host-only MQTT
  *     payload codec allocates its parse tree in host memory (freed by cfa_payload_free).
  *   - `stream` is a hipStream_t passed as void*; NULL means the legacy default stream.
- *     Every compute call is asynchronous on that stream.
+ *     Every compute call is asynchronous on that stream. Every device pointer of a call must be
+ *     memory of the stream's GPU: the library does not query pointer attributes on the launch
+ *     path, so another GPU's pointer is not refused here (the Python engine refuses such
+ *     tensors, federated_amd/engine.py _same_device).
  *   - Return 0 on success, a negative CFA_E* code on failure. `cfa_last_error()` returns a
  *     thread-local message for the last failure on the calling thread. No exceptions cross
  *     the ABI. Calls are re-entrant and thread-safe. The one piece of process-wide state is the
