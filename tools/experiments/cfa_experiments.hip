@@ -1053,6 +1053,84 @@ __global__ __launch_bounds__(kBlock) void mewma64_sm_kernel(XMewma a, long long 
   }
 }
 
+// Software-pipelined form of mewma64_x_kernel (round 4): the loads of a workgroup's next tile are
+// issued BEFORE the current tile is computed and stored. vmcnt counts loads and stores together in
+// issue order (MI355X_MICROARCH.md), so in the plain loop the first use of tile t+1's loads also
+// waits for every store of tile t; here the stores of tile t are younger than tile t+1's loads
+// and the wait leaves them in flight. Two tiles of registers per lane.
+template <int N, int U>
+struct MewmaTile {
+  xd2 W[U], g[U][N], s[U][N];
+};
+template <int N, int U, bool NTL>
+__device__ __forceinline__ void mewma_tile_load(MewmaTile<N, U>& T, const XMewma& a, long long base) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * kBlock;
+    T.W[u] = x_load<NTL>(reinterpret_cast<const xd2*>(a.W), i);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      T.g[u][j] = x_load<true>(reinterpret_cast<const xd2*>(a.g[j]), i);
+      T.s[u][j] = x_load<NTL>(reinterpret_cast<const xd2*>(a.s[j]), i);
+    }
+  }
+}
+template <int N, int U, int SP>
+__device__ __forceinline__ void mewma_tile_store(MewmaTile<N, U>& T, const XMewma& a, long long base,
+                                                 __amdgpu_buffer_rsrc_t wr, const __amdgpu_buffer_rsrc_t (&sr)[N]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * kBlock;
+    x_mewma<N>(T.W[u], T.g[u], T.s[u], 2 * i, a);
+#pragma unroll
+    for (int j = 0; j < N; ++j) x_store<xd2, SP>(reinterpret_cast<xd2*>(a.s[j]), sr[j], i, T.s[u][j]);
+    x_store<xd2, SP>(reinterpret_cast<xd2*>(a.W), wr, i, T.W[u]);
+  }
+}
+template <int N, int U, int SP, bool NTL>
+__global__ __launch_bounds__(kBlock) void mewma64_pipe_kernel(XMewma a, long long nvec2) {
+  constexpr long long kTile = (long long)kBlock * U;
+  const long long full = nvec2 / kTile;
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, (unsigned)(nvec2 * 16), 0x00020000);
+  __amdgpu_buffer_rsrc_t sr[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) sr[j] = __builtin_amdgcn_make_buffer_rsrc((void*)a.s[j], 0, (unsigned)(nvec2 * 16), 0x00020000);
+  long long t = blockIdx.x;
+  if (t < full) {
+    MewmaTile<N, U> A, B;
+    mewma_tile_load<N, U, NTL>(A, a, t * kTile + threadIdx.x);
+    // two tiles per trip, A and B alternating, so no register copies between the roles. The next
+    // tile's loads are unconditional (past the last tile they re-read the current one, whose values
+    // are then discarded): a load behind a branch makes the wait after the join a vmcnt(0).
+    for (;;) {
+      const long long t1 = t + gridDim.x;
+      mewma_tile_load<N, U, NTL>(B, a, (t1 < full ? t1 : t) * kTile + threadIdx.x);
+      mewma_tile_store<N, U, SP>(A, a, t * kTile + threadIdx.x, wr, sr);
+      if (t1 >= full) break;
+      const long long t2 = t1 + gridDim.x;
+      mewma_tile_load<N, U, NTL>(A, a, (t2 < full ? t2 : t1) * kTile + threadIdx.x);
+      mewma_tile_store<N, U, SP>(B, a, t1 * kTile + threadIdx.x, wr, sr);
+      if (t2 >= full) break;
+      t = t2;
+    }
+  }
+  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
+    xd2* W2 = reinterpret_cast<xd2*>(a.W);
+    for (long long i = full * kTile + threadIdx.x; i < nvec2; i += kBlock) {
+      xd2 Wv = W2[i], g[N], s[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        g[j] = reinterpret_cast<const xd2*>(a.g[j])[i];
+        s[j] = reinterpret_cast<const xd2*>(a.s[j])[i];
+      }
+      x_mewma<N>(Wv, g, s, 2 * i, a);
+#pragma unroll
+      for (int j = 0; j < N; ++j) reinterpret_cast<xd2*>(a.s[j])[i] = s[j];
+      W2[i] = Wv;
+    }
+  }
+}
+
 template <int U, int SP, bool NTL>
 __global__ __launch_bounds__(kBlock) void compress_full_kernel(float* y, const float* ref, long long nvec,
                                                               CompressParams cp) {
@@ -1148,6 +1226,12 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mewma64(
   if (u == U && sp == S + 10 && ntl == L) { mewma64_sm_kernel<2, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec2); return check_launch("mewma64_sm"); }
   CFA_SM(1, 1, 1) CFA_SM(2, 1, 1) CFA_SM(4, 1, 1) CFA_SM(4, 3, 1) CFA_SM(2, 3, 1) CFA_SM(4, 2, 1)
 #undef CFA_SM
+  // sp + 20: software-pipelined (mewma64_pipe_kernel)
+#define CFA_PI(U, S, L) \
+  if (u == U && sp == S + 20 && ntl == L) { mewma64_pipe_kernel<2, U, S, L><<<grid, kBlock, 0, st>>>(a, nvec2); return check_launch("mewma64_pipe"); }
+  CFA_PI(1, 1, 1) CFA_PI(2, 1, 1) CFA_PI(1, 3, 1) CFA_PI(2, 3, 1) CFA_PI(1, 2, 1) CFA_PI(2, 2, 1) CFA_PI(4, 3, 1)
+  CFA_PI(1, 0, 0) CFA_PI(2, 0, 0)
+#undef CFA_PI
   return fail(CFA_E_INVALID, "mewma64 variant not instantiated");
 }
 

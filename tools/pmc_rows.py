@@ -39,6 +39,8 @@ ROWS = {
     "compress_epilogue_mode2": ("cfa_compress_epilogue_f32", lambda P: 3 * P * 4, lambda P: P),
     "fold_f64_div_n4": ("cfa_fold_f64", lambda P: 6 * P * 8, lambda P: P),
     "mewma_tf1_f64_n2": ("cfa_mewma_tf1_f64", lambda P: 8 * P * 8, lambda P: P),
+    "mix_tf1_n8": ("cfa_mix_tf1_f32", lambda P: 10 * P * 4, lambda P: P),
+    "mix_tf1_wide_n8": ("cfa_mix_tf1_wide_f32", lambda P: 9 * P * 4 + P * 8, lambda P: P),
 }
 PASSES = [
     ("fetch", ["FETCH_SIZE"]),
@@ -71,6 +73,15 @@ def child(name, P, reps):
     elif name == "mewma_tf1_f64_n2":
         W64, s64, g64 = f64(), [f64() for _ in range(2)], [f64() for _ in range(2)]
         fn = lambda: eng.mewma_tf1_f64(W64, s64, g64, 0.99, 0.1, 0.1, P // 2, False, True)
+    elif name == "mix_tf1_n8":
+        local, out, nb = f32(), torch.empty(P, device="cuda"), [f32() for _ in range(8)]
+        fn = lambda: eng.mix_tf1(out, local, nb, [1.0 / 9] * 8)
+    elif name == "mix_tf1_wide_n8":
+        local, nb = f32(), [f32() for _ in range(8)]
+        o64 = torch.empty(P, device="cuda", dtype=torch.float64)
+        tb, al64 = _lib.ptr_table([x.data_ptr() for x in nb]), _lib.double_array([1.0 / 9] * 8)
+        fn = lambda: _lib.call("cfa_mix_tf1_wide_f32", o64.data_ptr(), local.data_ptr(), tb, al64, 8, P, 0, 0, 0,
+                               None, eng.stream_handle())
     else:
         raise SystemExit(f"unknown kernel row {name}")
     for _ in range(2):

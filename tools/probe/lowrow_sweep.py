@@ -142,7 +142,11 @@ def main():
                                 (1, 4, 2, 1),
                                 # sp + 10: stream-major load / store order (mewma64_sm_kernel)
                                 (1, 1, 11, 1), (1, 2, 11, 1), (1, 4, 11, 1), (1, 4, 13, 1), (2, 4, 13, 1),
-                                (4, 4, 13, 1), (2, 2, 13, 1), (1, 4, 12, 1), (2, 4, 11, 1)]:
+                                (4, 4, 13, 1), (2, 2, 13, 1), (1, 4, 12, 1), (2, 4, 11, 1),
+                                # sp + 20: software-pipelined (mewma64_pipe_kernel, round 4)
+                                (1, 1, 21, 1), (2, 1, 21, 1), (1, 2, 21, 1), (1, 1, 23, 1), (2, 1, 23, 1),
+                                (1, 2, 23, 1), (2, 2, 23, 1), (1, 1, 22, 1), (2, 1, 22, 1), (4, 1, 21, 1),
+                                (1, 4, 23, 1), (1, 1, 20, 0), (2, 1, 20, 0)]:
             fn = (lambda bpc=bpc, u=u, sp=sp, ntl=ntl: call(
                 "cfa_experimental_mewma64", vp(W.data_ptr()), st, gt, ctypes.c_double(rho), ctypes.c_double(lr1),
                 ctypes.c_double(lr2), ctypes.c_size_t(split), 1, ctypes.c_size_t(P), u, sp, ntl, bpc, vp(sh)))
