@@ -30,20 +30,32 @@ struct Tf1Fanin {
 // pass (no epilogue), or the unrounded fp64 result (epilogue in fp64, no rounding).
 enum { kOutF32 = 0, kOutScratch64 = 1, kOutF64 = 2 };
 
-// One float4 of the TF1 chain: x = the N neighbour vectors, l = the local vector, w64 = the
+// Vector width of the TF1 kernel: float4 per lane for the fp32 output (16-B loads, 16-B stores);
+// float2 for the fp64 outputs, so that each lane's result is ONE 16-byte store and a wave's store
+// instruction covers 1 KiB contiguously. (With float4 per lane the four fp64 results are two
+// 16-B stores at a 32-B lane stride: each store instruction half-fills 16 lines and the other
+// half follows in the next instruction.)
+template <int OUT>
+struct Tf1Vec {
+  static constexpr int W = OUT == kOutF32 ? 4 : 2;
+  typedef float type __attribute__((ext_vector_type(W)));
+};
+
+// One vector of the TF1 chain: x = the N neighbour vectors, l = the local vector, w64 = the
 // previous pass's running fp64 w (FROM64), i = the vector's index. Epilogue, rounding and store.
-template <int N, bool FROM64, int OUT>
-__device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fanin& f, const f4 (&x)[N],
-                                        const f4& l, const double* w64, long long i, const CompressParams& cp,
+template <int N, bool FROM64, int OUT, typename V = typename Tf1Vec<OUT>::type>
+__device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fanin& f, const V (&x)[N],
+                                        const V& l, const double* w64, long long i, const CompressParams& cp,
                                         int compress, unsigned& kept) {
-  double w[4];
+  constexpr int W = Tf1Vec<OUT>::W;
+  double w[W];
   constexpr int j0 = FROM64 ? 0 : 1;
   if constexpr (FROM64) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[c] = w64[c];
+    for (int c = 0; c < W; ++c) w[c] = w64[c];
   } else {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < W; ++c) {
       const float d = x[0][c] - l[c];            // fp32 - fp32 (both operands fp32)
       w[c] = (double)l[c] + f.a[0] * (double)d;  // np.float64 * fp32 -> fp64; fp32 + fp64 -> fp64
     }
@@ -51,48 +63,51 @@ __device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fan
 #pragma unroll
   for (int j = j0; j < N; ++j)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
+    for (int c = 0; c < W; ++c) w[c] = w[c] + f.a[j] * ((double)x[j][c] - w[c]);
   if (OUT != kOutScratch64 && compress) {
-    const long long e0 = i * 4;
+    const long long e0 = i * W;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < W; ++c)
       if (e0 + c >= cp.cbegin && e0 + c < cp.cend) w[c] = compress_one_d(w[c], l[c], cp, kept);
   }
   if constexpr (OUT == kOutF32) {
     const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
     st16_sc1(o, i, y);
-  } else {  // fp64 out: plain stores (two sc1 halves per lane measured 17% slower)
-    double* od = reinterpret_cast<double*>(out) + 4 * i;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) od[c] = w[c];
+  } else {  // fp64 out: one plain 16-B store per lane (sc1 halves measured 17% slower in round 2)
+    const d2 y = {w[0], w[1]};
+    reinterpret_cast<d2*>(out)[i] = y;
   }
 }
 
-// Full tiles of kBlock * U float4 per block (grid-stride over tiles, every load of a tile issued
+// Full tiles of kBlock * U vectors per block (grid-stride over tiles, every load of a tile issued
 // before its first use, nontemporal loads), the partial last tile by the block that owns it with
-// per-vector guards: the headline mix's skeleton (round 4).
+// per-vector guards: the headline mix's skeleton (round 4). nvec counts vectors of Tf1Vec<OUT>::W
+// elements.
 template <int N, bool FROM64, int OUT, int U>
 __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin f, long long nvec,
                                                               CompressParams cp, int compress) {
+  using V = typename Tf1Vec<OUT>::type;
+  constexpr int W = Tf1Vec<OUT>::W;
   constexpr long long kTile = (long long)kBlock * U;
   unsigned kept = 0;
-  const Sc1Out o = sc1_out(out, nvec * 16);  // used by the fp32 output only
+  const Sc1Out o = sc1_out(out, nvec * 16);  // used by the fp32 output only (16-B vectors)
   const long long full = nvec / kTile;
+  auto ld = [](const float* p, long long i) { return __builtin_nontemporal_load(reinterpret_cast<const V*>(p) + i); };
   for (long long t = blockIdx.x; t < full; t += gridDim.x) {
     const long long base = t * kTile + threadIdx.x;
-    f4 x[U][N], l[U];
+    V x[U][N], l[U];
 #pragma unroll
     for (int k = 0; k < N; ++k)
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
+      for (int u = 0; u < U; ++u) x[u][k] = ld(f.src[k], base + (long long)u * kBlock);
 #pragma unroll
-    for (int u = 0; u < U; ++u) l[u] = ld4<true>(f.local, base + (long long)u * kBlock);
-    double w64[U][4];
+    for (int u = 0; u < U; ++u) l[u] = ld(f.local, base + (long long)u * kBlock);
+    double w64[U][W];
     if constexpr (FROM64) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) w64[u][c] = f.w64[4 * (base + (long long)u * kBlock) + c];
+        for (int c = 0; c < W; ++c) w64[u][c] = f.w64[W * (base + (long long)u * kBlock) + c];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -100,14 +115,14 @@ __global__ __launch_bounds__(kBlock) void mix_tf1_vec_kernel(void* out, Tf1Fanin
   }
   if (blockIdx.x == (unsigned)(full % gridDim.x)) {
     for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
-      f4 x[N];
+      V x[N];
 #pragma unroll
-      for (int k = 0; k < N; ++k) x[k] = ld4<true>(f.src[k], i);
-      const f4 l = ld4<true>(f.local, i);
-      double w64[4];
+      for (int k = 0; k < N; ++k) x[k] = ld(f.src[k], i);
+      const V l = ld(f.local, i);
+      double w64[W];
       if constexpr (FROM64) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) w64[c] = f.w64[4 * i + c];
+        for (int c = 0; c < W; ++c) w64[c] = f.w64[W * i + c];
       }
       tf1_vec<N, FROM64, OUT>(out, o, f, x, l, w64, i, cp, compress, kept);
     }
@@ -420,13 +435,16 @@ static void launch_tf1_vec_u(int n, unsigned grid, hipStream_t st, void* out, co
 // CFA_BLOCKS_PER_CU. Default (round 4, tools/kernel_rooflines.py A/B, two alternated rounds on one
 // box, profiles/r04_tf1_ab_rooflines.jsonl): fp32 out two float4 per lane at two workgroups per CU
 // (0.782 / 0.783 of peak at 25M, n = 8, against 0.757 / 0.755 for the one-vector grid-stride
-// kernel before; one float4: 0.743, four: 0.757); fp64 out four float4 at one workgroup per CU
-// (0.751 / 0.757 against 0.754 / 0.754 before; two float4: 0.668, one: 0.746).
+// kernel before; one float4: 0.743, four: 0.757); fp64 out four float2 at one workgroup per CU
+// (profiles/r04_tf1b_ab_rooflines.jsonl: 0.781 / 0.781 against 0.754 / 0.755 for four float4,
+// whose fp64 results left as two 16-B stores at a 32-B lane stride; float2 with two: 0.759 / 0.753,
+// one: 0.701 / 0.711; two workgroups per CU with four: 0.755 / 0.757, with two: 0.719 / 0.730).
 template <bool FROM64, int OUT>
 static void launch_tf1_vec(int n, hipStream_t st, void* out, const Tf1Fanin& f, long long nvec,
                            const CompressParams& cp, int compress) {
   const cfa_launch_t& t = tune();
   const int U = t.vec_per_lane > 0 ? norm_vec(t.vec_per_lane) : (OUT == kOutF32 ? 2 : 4);
+  nvec *= 4 / Tf1Vec<OUT>::W;  // the caller counts float4; the fp64 outputs run float2 vectors
   const long long tiles = (nvec + (long long)kBlock * U - 1) / ((long long)kBlock * U);
   const unsigned grid = OUT == kOutF64 ? grid_for_own(tiles, 1) : grid_for(tiles);
   if (U == 4) launch_tf1_vec_u<FROM64, OUT, 4>(n, grid, st, out, f, nvec, cp, compress);
