@@ -21,6 +21,10 @@ from oracle import cfa_oracle as O
 
 pytestmark = pytest.mark.gpu
 
+# CFA_DROPIN_FUZZ_CASES (default 6) seeds per drop-in class; CFA_DROPIN_FUZZ_SEED shifts them
+SEEDS = [int(os.environ.get("CFA_DROPIN_FUZZ_SEED", "0")) + k
+         for k in range(int(os.environ.get("CFA_DROPIN_FUZZ_CASES", "6")))]
+
 
 @pytest.fixture
 def workdir(tmp_path, monkeypatch):
@@ -50,7 +54,7 @@ def _same(got, want):
     return got.dtype == want.dtype and np.array_equal(got.reshape(want.shape), want)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", SEEDS)
 def test_tf1_cfa_dropin_random(workdir, seed):
     from federated_amd.consensus.cfa import CFA_process
     rng = np.random.default_rng(9700 + seed)
@@ -77,7 +81,7 @@ def test_tf1_cfa_dropin_random(workdir, seed):
             assert _same(res[t], np.asarray(want[t])), (K, N, ii, t)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", SEEDS)
 def test_tf1_ongraphs_mode1_dropin_random(workdir, seed):
     from federated_amd.consensus.cfa_ongraphs import CFA_process
     rng = np.random.default_rng(9800 + seed)
@@ -110,7 +114,7 @@ def test_tf1_ongraphs_mode1_dropin_random(workdir, seed):
     assert res[4] == counter, (K, ii, nb, comp)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", SEEDS)
 def test_tf2_dropin_random(workdir, seed):
     from federated_amd.consensus import consensus_v3, consensus_v4
     rng = np.random.default_rng(9900 + seed)
@@ -147,7 +151,7 @@ def test_tf2_dropin_random(workdir, seed):
         assert _same(res_g[t], want_g[t]), (D, n, "grads", t)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", SEEDS)
 def test_parameter_server_v2_dropin_random(workdir, seed):
     from federated_amd.consensus import parameter_server_v2
     rng = np.random.default_rng(10000 + seed)
