@@ -160,8 +160,8 @@ def wait_for_status(seconds: float) -> None:
     """A rank other than 0 about to leave early: wait until rank 0 has recorded the run's status
     (self-launched runs), else ``seconds``, so rank 0 is not ended before its line is printed."""
     path = os.environ.get(STATUS_FILE_ENV)
-    end = time.time() + seconds
-    while time.time() < end:
+    end = time.monotonic() + seconds
+    while time.monotonic() < end:
         if path and os.path.exists(path):
             time.sleep(0.5)  # the line is printed before the status is recorded
             return
@@ -169,17 +169,25 @@ def wait_for_status(seconds: float) -> None:
 
 
 def run_origin() -> float:
-    """Epoch seconds the run started: the self-launching parent's start when there is one."""
+    """Epoch seconds the run started: the self-launching parent's start when there is one. Only
+    handed between the parent and the ranks; every deadline is measured on the monotonic clock
+    from ``monotonic_origin`` (a stepped system clock moves neither)."""
     try:
         return float(os.environ[T0_ENV])
     except (KeyError, ValueError):
         return time.time()
 
 
-class Budget:
-    """The whole run's time budget (``--total-seconds``) from ``t0`` (epoch seconds)."""
+def monotonic_origin(t0_epoch: float) -> float:
+    """The run's origin on ``time.monotonic``'s scale: the epoch origin converted once, at start-up."""
+    return time.monotonic() - max(0.0, time.time() - float(t0_epoch))
 
-    def __init__(self, total: float, t0: float = None, clock=time.time):
+
+class Budget:
+    """The whole run's time budget (``--total-seconds``) from ``t0`` (on ``clock``'s scale: monotonic
+    seconds, see ``monotonic_origin``)."""
+
+    def __init__(self, total: float, t0: float = None, clock=time.monotonic):
         self.total, self.clock = float(total), clock
         self.t0 = clock() if t0 is None else float(t0)
 
@@ -235,14 +243,14 @@ class Watchdog:
     def __init__(self, seconds: float, rank: int, t0: float = None):
         import threading
         self.phase, self.rank, self._done = "start-up", rank, threading.Event()
-        self.t0 = time.time() if t0 is None else t0
+        self.t0 = time.monotonic() if t0 is None else t0  # monotonic scale (monotonic_origin)
         self._leg = None  # (deadline, budget, on_expire) of a phase entered with its own budget
         self.seconds = seconds
         threading.Thread(target=self._watch, daemon=True).start()
 
     def _watch(self):
         while not self._done.wait(0.25):
-            now = time.time()
+            now = time.monotonic()
             leg = self._leg
             if leg is not None and now > leg[0]:
                 print(f"[bench rank {self.rank}] watchdog: phase '{self.phase}' did not finish within its "
@@ -266,7 +274,7 @@ class Watchdog:
         headline is already measured, so a leg stuck in a collective is reported in the line instead
         of losing the whole run)."""
         self.phase = phase
-        self._leg = (time.time() + budget, budget, on_expire) if budget > 0 else None
+        self._leg = (time.monotonic() + budget, budget, on_expire) if budget > 0 else None
 
     def end_leg(self) -> None:
         self._leg = None
@@ -693,7 +701,7 @@ def main():
         # the ranks are this script's children (torch.distributed.run), started before anything
         # here touches the GPU; this process only relays their line and status
         sys.exit(self_launch(sys.argv[1:], args.gpus, args.total_seconds))
-    t0 = run_origin()
+    t0 = monotonic_origin(run_origin())
     budget = Budget(args.total_seconds, t0)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -832,7 +840,7 @@ def main():
         watchdog.enter("timed rounds")
         return (xshard, xinfo, xtune) + run_leg(args, xshard, world, args.steps, args.warmup)
 
-    t_head0 = time.time()
+    t_head0 = time.perf_counter()
     if world == 1:
         shard, info, autotune, elapsed, durations, launches_per_step = measure_headline(headline)
     else:
@@ -868,7 +876,7 @@ def main():
     if reuse and not args.window_batch and len(interior) > 1:
         watchdog.enter("timed rounds, scattered order")
         scat = timed_scattered(shard, args.steps)
-    t_headline = time.time() - t_head0
+    t_headline = time.perf_counter() - t_head0
 
     result = None
     if rank == 0:
@@ -1043,7 +1051,7 @@ def main():
             watchdog.leg(f"{name} leg", seconds, leg_expired(name, seconds))
             leg, err = {"note": notes[name]}, None
             xshard = None
-            t_leg = time.time()
+            t_leg = time.perf_counter()
             try:
                 if part != "params" and ensure_transport() is None:
                     raise TransportError(tstate["error"])
@@ -1077,7 +1085,7 @@ def main():
                 if part != "params":
                     leg["transport"] = tstate["transport"].name
                     leg["comparable"] = tstate["comparable"]
-                leg["wall_s"] = round(time.time() - t_leg, 1)
+                leg["wall_s"] = round(time.perf_counter() - t_leg, 1)
             except Exception as exc:  # reported in the line; every rank takes the same decision below
                 err = f"{type(exc).__name__}: {exc}"
                 print(f"[bench rank {rank}] {name} leg failed: {err}", file=sys.stderr, flush=True)

@@ -206,7 +206,8 @@ def load_experiments() -> ctypes.CDLL:
     with _lock:
         if _exp is None:
             if not os.path.isfile(EXP_PATH):
-                raise ImportError(f"{EXP_PATH} not found; build it with `make -C federated_amd/csrc`")
+                raise ImportError(f"{EXP_PATH} not found; build it with `make -C federated_amd/csrc exp` "
+                                  "(not part of the product build)")
             _exp = ctypes.CDLL(EXP_PATH, mode=ctypes.RTLD_LOCAL)
             _exp.cfa_exp_last_error.restype = ctypes.c_char_p
     return _exp

@@ -176,24 +176,32 @@ struct Fanin {
   double rd[CFA_MAX_FANIN + 1];         // SEQ_DIV: rd[j] = RN_64(1 / d[j]) (div4_rn)
 };
 
-// Correctly rounded fp32 a / b as ONE fp64 multiply: (float)((double)a * RN_64(1/b)) is exactly
-// IEEE a / b for every fp32 a and b, with no range guard. The exact quotient of two 24-bit
-// significands lies at least 2^-48 (relative) from every fp32 rounding midpoint, normal or
-// subnormal, while the two fp64 roundings (of 1/b and of the product) stay within 2^-52 of it;
-// fp64's exponent range holds every fp32 quotient (so fp32 overflow and underflow happen in the
-// final conversion, as in the IEEE division), and zeros, infinities and NaN propagate as they do
-// there (0 * inf = NaN for 0/0, x * 0 = 0 for x/inf). Two conversions and one v_mul_f64 per
-// element, branch-free; round 4 replaced Markstein's three fp32 operations plus a range test per
-// float4 with it (tools/probe/lowrow_sweep.py --only div, profiles/r04_div64_sweep.jsonl: 0.733 ->
-// 0.776 of peak at 25M, n = 8). Tested bit for bit against numpy over every binade
-// (tests/test_gpu_div.py; 10^8 random bit patterns on the CPU, tests/test_div64_rule.py).
-__device__ __forceinline__ float div_rd(float a, double rb) { return (float)((double)a * rb); }
-__device__ __forceinline__ f4 div4_rn(f4 a, double rb) {
+// Correctly rounded fp32 a / b as one fp64 multiply: p = (double)a * RN_64(1/b) rounded to fp32
+// is IEEE a / b whenever the quotient is a NORMAL fp32 (or zero, infinite, NaN). The exact
+// quotient of two 24-bit significands then lies at least 2^-48 (relative) from every fp32
+// rounding midpoint, while the two fp64 roundings (of 1/b and of the product) stay within 2^-52
+// of it; fp64's exponent range holds every fp32 quotient, so overflow happens in the final
+// conversion as in the IEEE division, and zeros, infinities and NaN propagate as they do there
+// (0 * inf = NaN for 0/0, x * 0 = 0 for x/inf). A SUBNORMAL quotient has fewer significand bits
+// and can sit exactly on a midpoint (a = odd k * o * 2^-149, b = 2o): there the fp64 error of
+// RN(1/b) decides the rounding instead of ties-to-even, so 0 < |p| < 2^-126 takes the IEEE fp32
+// division (never on the bench's buckets; the lanes that take it are exec-masked). Round 4
+// replaced Markstein's three fp32 operations plus a range test per float4 with the one-multiply
+// form (profiles/r04_div64_sweep.jsonl: 0.733 -> 0.776 of peak at 25M, n = 8). Tested bit for
+// bit against numpy over every binade and on exact subnormal ties (tests/test_gpu_kernels.py
+// test_mix_seq_div_*; the rule itself on the CPU, tests/test_div64_rule.py).
+__device__ __forceinline__ float div_rd(float a, double rb, float b) {
+  const double p = (double)a * rb;
+  const double m = __builtin_fabs(p);
+  if (m < 0x1p-126 && m != 0.0) return a / b;
+  return (float)p;
+}
+__device__ __forceinline__ f4 div4_rn(f4 a, double rb, float b) {
   f4 q;
-  q.x = div_rd(a.x, rb);
-  q.y = div_rd(a.y, rb);
-  q.z = div_rd(a.z, rb);
-  q.w = div_rd(a.w, rb);
+  q.x = div_rd(a.x, rb, b);
+  q.y = div_rd(a.y, rb, b);
+  q.z = div_rd(a.z, rb, b);
+  q.w = div_rd(a.w, rb, b);
   return q;
 }
 
@@ -232,7 +240,7 @@ __device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
     for (int j = 1; j <= N; ++j) {
       f4 t = v[j] - w;  // numpy: (x - w)
       t = f.c[j] * t;   //        u * (...)
-      t = div4_rn(t, f.rd[j]);  // (...) / C, IEEE-correct fp32 division
+      t = div4_rn(t, f.rd[j], f.d[j]);  // (...) / C, IEEE-correct fp32 division
       w = w + t;
     }
     return w;

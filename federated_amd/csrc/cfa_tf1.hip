@@ -73,9 +73,15 @@ __device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fan
   if constexpr (OUT == kOutF32) {
     const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
     st16_sc1(o, i, y);
-  } else {  // fp64 out: one plain 16-B store per lane (sc1 halves measured 17% slower in round 2)
+  } else if ((reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    // fp64 out: one plain 16-B store per lane (sc1 halves measured 17% slower in round 2); only
+    // on a 16-B aligned bucket (a uniform test of the kernel argument)
     const d2 y = {w[0], w[1]};
     reinterpret_cast<d2*>(out)[i] = y;
+  } else {  // an fp64 view that starts at an odd element: the bucket is only 8-B aligned
+    double* q = reinterpret_cast<double*>(out) + 2 * i;
+    q[0] = w[0];
+    q[1] = w[1];
   }
 }
 

@@ -35,29 +35,50 @@
  *     allocation on the launch path (cfa_mix_tf1_f32 above CFA_MAX_FANIN refuses capture and
  *     points to cfa_mix_tf1_ex_f32), so captures run in the strict (global) mode.
  *
- * Where the ABI departs from the signatures sketched in SURVEY.md §8(b), and why
- *   - cfa_mix_f32 / cfa_mix_seq_f32: (out, local, nbrs, coeff, n, P, stream) as sketched; the
- *     sequential rule is its own entry (alphas, not closed-form coefficients) because the
- *     reference's fp32 chain is three roundings per step, which no coefficient vector reproduces.
- *   - cfa_compress_epilogue_f32 takes `mode` instead of (thr, rep): the four (thr, rep) pairs are
- *     fixed by cfa_ongraphs.py:225-273 and the mode also selects the sparse vs DPCM test, which
- *     (thr, rep) alone cannot express; a mode makes an inconsistent triple unrepresentable.
- *   - cfa_mix_population_f32 takes device tables of bucket pointers (out_ptrs, src_ptrs) instead
- *     of dense stacks: a population's devices live in separate buffers (ping-pong models, halo
- *     rows, per-device allocations from callers) and a pointer table serves all of them with one
- *     launch; a dense [D, P] stack is the special case (cfa_mix_ring_round_f32 takes one).
- *   - cfa_comm_init(comm, rank, nranks, id, device): the communicator comes back through an out
- *     parameter so the return value stays the status code like every other entry, and `device`
- *     is explicit so a caller thread need not have selected the GPU beforehand.
- *   - cfa_mix_strided_f32 (sketched for the `[..., devices]` gradient slices of CFA-GE,
- *     cfa_ge_2stage.py:594-606) is not provided. Those slices arrive in host memory (loadmat),
- *     and the host mixer gathers slot `ii` while packing the pinned staging rows, so every GPU
- *     read is a coalesced row. Read on the device, a stride-D slice pulls a whole line per 4
- *     useful bytes: the round-1 entry ran at 0.31 of peak with 2.5x over-fetch, so it was
- *     retired in round 2 instead of being exposed.
- *   - cfa_halo_exchange_f32 is joined by cfa_p2p_group_f32, with per-message counts, for the routed,
- *     chunked halo; cfa_allreduce_scaled_f32 became cfa_allreduce_sum_f32 / cfa_reduce_sum_f32
- *     because the pre-scaling is fused into the mix that produces the buffer (one pass fewer).
+ * Where the ABI departs from the signatures sketched in SURVEY.md §8(b), entry by entry
+ * (tests/test_capi.py holds the sketch's parameter lists and checks every prototype below
+ * against this list)
+ *   - cfa_mix_f32(out, local, nbrs, coeff, n, P, stream): `coeff` and `n` are SWAPPED relative to
+ *     the sketch's (out, local, nbrs, n, coeff, P, stream), so that every mix entry reads
+ *     (out, local, nbrs, <per-neighbour host array>, n, P, ...) alike: cfa_mix_seq_f32 and
+ *     cfa_mix_seq_div_f32 take alphas (and divisors) in that same slot. A C caller following the
+ *     sketch must swap the two. The sequential rule is its own entry (alphas, not closed-form
+ *     coefficients) because the reference's fp32 chain is three roundings per step, which no
+ *     coefficient vector reproduces.
+ *   - cfa_mewma_update_f32(W, s, g, g_stride, n, rho, lr1, lr2, lr_split, init, use_filtered, P,
+ *     stream) against the sketch's (W, s, g, n, rho, lr, use_filtered, P, stream):
+ *     `g_stride` (per-neighbour element stride of g_j, NULL = contiguous) reads the
+ *     `[..., devices]` gradient slices the sketch gave to cfa_mix_strided_f32; `rho` is a double
+ *     so rho and 1 - rho each round once to fp32 as numpy does with a Python float; the one `lr`
+ *     becomes (lr1, lr2, lr_split) because the reference applies -l1 to the layer-1 tensors and
+ *     -l2 to the layer-2 tensors of one bucket (federated_sample_CNN_CFA-GE.py:16-17,29-30);
+ *     `init` selects the 4-stage epoch-1 rule s_j <- g_j (cfa_ge_2stage.py:332-336).
+ *   - cfa_compress_epilogue_f32(y, ref, mode, P, kept_count, stream) against the sketch's
+ *     (y, ref_or_null, thr, rep, mode, kept_count, P, stream): `mode` replaces (thr, rep), since
+ *     the four (thr, rep) pairs are fixed by cfa_ongraphs.py:225-273 and the mode also selects the
+ *     sparse vs DPCM test, which (thr, rep) alone cannot express (a mode makes an inconsistent
+ *     triple unrepresentable); `P` comes before `kept_count`, the order of every sized entry here.
+ *   - cfa_mix_population_f32(out_ptrs, src_ptrs, csr_ptr, csr_idx, csr_coef, D, rule, P, stream)
+ *     against (out_stack, in_stack, csr_ptr, csr_idx, csr_coeff, D, P, stream): device tables of
+ *     bucket pointers instead of dense stacks, because a population's devices live in separate
+ *     buffers (ping-pong models, halo rows, per-device allocations from callers) and a pointer
+ *     table serves all of them with one launch (a dense [D, P] stack is the special case,
+ *     cfa_mix_ring_round_f32); `rule` added so one launch serves the sequential CFA rule and the
+ *     linear FedAvg form.
+ *   - cfa_comm_init(comm, rank, nranks, id, device) against (rank, nranks, id, comm): the
+ *     communicator out parameter comes first and `device` is added, so a caller thread need not
+ *     have selected the GPU beforehand; the return value stays the status code.
+ *   - cfa_mix_strided_f32 is not provided. The `[..., devices]` gradient slices of CFA-GE
+ *     (cfa_ge_2stage.py:594-606) arrive in host memory (loadmat), and the host mixer gathers slot
+ *     `ii` while packing the pinned staging rows, so every GPU read is a coalesced row. Read on
+ *     the device, a stride-D slice pulls a whole line per 4 useful bytes: the round-1 entry ran at
+ *     0.31 of peak with 2.5x over-fetch, so it was retired in round 2 (g_stride above keeps the
+ *     strided read for the MEWMA update, whose caller may hold such slices on the device).
+ *   - cfa_halo_exchange_f32, whose parameters the sketch elides, takes whole buckets; it is joined by
+ *     cfa_p2p_group_f32, with per-message counts, for the routed, chunked halo.
+ *     cfa_allreduce_scaled_f32 became cfa_allreduce_sum_f32 / cfa_reduce_sum_f32 because the
+ *     pre-scaling is fused into the mix that produces the buffer (one pass fewer).
+ *   - cfa_comm_destroy, cfa_last_error and cfa_version are as sketched.
  */
 #ifndef CFA_ENGINE_H
 #define CFA_ENGINE_H

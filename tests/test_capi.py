@@ -47,7 +47,7 @@ def test_ctypes_table_matches_header():
     assert sorted(_lib.SIGNATURES) == header_symbols()
     text = _header_text()
     for name, (_, args) in _lib.SIGNATURES.items():
-        m = re.search(r"\b%s\s*\(([^)]*)\)" % name, text, re.S)
+        m = re.search(r"CFA_API[^;(]*\b%s\s*\(([^)]*)\)" % name, text, re.S)
         decl = m.group(1).strip()
         nargs = 0 if decl in ("", "void") else decl.count(",") + 1
         assert nargs == len(args), name
@@ -127,3 +127,86 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+# SURVEY.md §8(b) "New C-ABI the shim must export": the sketched parameter lists (names only, in
+# order). None = the sketch elides the parameters ("(...)"); the entries it names but the library
+# does not provide map to None with the reason in the header's departures list.
+SKETCH_8B = {
+    "cfa_mix_f32": ["out", "local", "nbrs", "n", "coeff", "P", "hip_stream"],
+    "cfa_mix_strided_f32": None,  # sketched as "(..., nbr_stride)"; not provided
+    "cfa_mewma_update_f32": ["W", "s", "g", "n", "rho", "lr", "use_filtered", "P", "stream"],
+    "cfa_compress_epilogue_f32": ["y", "ref_or_null", "thr", "rep", "mode", "kept_count", "P", "stream"],
+    "cfa_mix_population_f32": ["out_stack", "in_stack", "csr_ptr", "csr_idx", "csr_coeff", "D", "P", "stream"],
+    "cfa_comm_init": ["rank", "nranks", "nccl_unique_id", "comm"],
+    "cfa_halo_exchange_f32": None,
+    "cfa_allreduce_scaled_f32": None,  # became cfa_allreduce_sum_f32 / cfa_reduce_sum_f32
+    "cfa_comm_destroy": ["comm"],
+    "cfa_last_error": [],
+    "cfa_version": [],
+}
+
+# The library's parameter lists for the same entries (what include/cfa_engine.h must declare).
+ABI_8B = {
+    "cfa_mix_f32": ["out", "local", "nbrs", "coeff", "n", "P", "stream"],
+    "cfa_mewma_update_f32": ["W", "s", "g", "g_stride", "n", "rho", "lr1", "lr2", "lr_split", "init",
+                             "use_filtered", "P", "stream"],
+    "cfa_compress_epilogue_f32": ["y", "ref", "mode", "P", "kept_count", "stream"],
+    "cfa_mix_population_f32": ["out_ptrs", "src_ptrs", "csr_ptr", "csr_idx", "csr_coef", "D", "rule", "P",
+                               "stream"],
+    "cfa_comm_init": ["comm", "rank", "nranks", "id", "device"],
+    "cfa_halo_exchange_f32": ["comm", "send_bufs", "send_peers", "nsend", "recv_bufs", "recv_peers", "nrecv",
+                              "P", "stream"],
+    "cfa_comm_destroy": ["comm"],
+    "cfa_last_error": [],
+    "cfa_version": [],
+}
+
+# Names the sketch and the ABI give the same parameter.
+_SAME = {"hip_stream": "stream", "nccl_unique_id": "id", "ref_or_null": "ref", "csr_coeff": "csr_coef"}
+
+
+def _prototype_params(name):
+    m = re.search(r"CFA_API[^;(]*\b%s\s*\(([^)]*)\)\s*;" % name, _header_text(), re.S)
+    assert m, name
+    decl = " ".join(m.group(1).split())
+    if decl in ("", "void"):
+        return []
+    return [re.findall(r"(\w+)\s*$", p.strip())[0] for p in decl.split(",")]
+
+
+def _departures():
+    text = _header_text()
+    start = text.index("Where the ABI departs from the signatures sketched")
+    return text[start:text.index("*/", start)]
+
+
+@pytest.mark.parametrize("name", sorted(ABI_8B))
+def test_prototype_parameter_order_against_survey_8b(name):
+    """Every entry SURVEY §8(b) sketches: the header's prototype has exactly the parameter order of
+    ABI_8B, and where that order differs from the sketch (beyond a renamed parameter) the entry is
+    named in the header's departures list, with every sketch parameter it drops or moves."""
+    got = _prototype_params(name)
+    assert got == ABI_8B[name], (name, got)
+    sketch = SKETCH_8B[name]
+    norm = [_SAME.get(p, p) for p in sketch] if sketch is not None else None
+    deps = _departures()
+    if norm is None or norm != got:
+        assert re.search(r"- %s\b" % name, deps) or name in deps, f"{name} departs from §8(b) silently"
+    if norm is not None and norm != got:
+        # the departure text names the entry's own full parameter list, in order
+        assert "%s(%s)" % (name, ", ".join(got)) in " ".join(deps.replace("*", " ").split()), name
+
+
+def test_sketched_entries_not_provided_are_explained():
+    exported = set(header_symbols())
+    deps = _departures()
+    for name, params in SKETCH_8B.items():
+        if name not in exported:
+            assert name in deps, f"{name} (sketched in SURVEY §8(b)) is neither exported nor explained"
+
+
+def test_mix_f32_swap_is_stated():
+    """Round-4 review: the header claimed cfa_mix_f32 was 'as sketched' while it swaps n and coeff."""
+    deps = " ".join(_departures().replace("*", " ").split())
+    assert "SWAPPED" in deps and "(out, local, nbrs, n, coeff, P, stream)" in deps

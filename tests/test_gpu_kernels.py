@@ -615,6 +615,26 @@ def test_mix_seq_div_quotient_exact_over_exponent_range(gpu, divisors):
             assert same.all(), (C, x[~same][:4], got[~same][:4], ref[~same][:4])
 
 
+@pytest.mark.parametrize("o", [49, 75, 77, 1, 3, 1023, 4095])
+def test_mix_seq_div_exact_subnormal_ties(gpu, o):
+    """Quotients exactly on a subnormal rounding midpoint (round-4 advisor finding): x = k * o *
+    2^-149 for odd k, C = 2 o, so x / C = (k / 2) * 2^-149 and ties-to-even decides. The fold's
+    one-multiply division alone rounds some of these the wrong way; div_rd sends 0 < |p| < 2^-126 to
+    the IEEE division. Random bit patterns (the test above) practically never hit these."""
+    k = np.arange(1, 1 << 15, 2, dtype=np.float64)
+    k = k[k * o < 2 ** 24]
+    x = np.concatenate([k * o * 2.0 ** -149, -(k * o * 2.0 ** -149)]).astype(np.float32)
+    x = np.concatenate([x, np.zeros((-x.size) % 64 + 64, np.float32)])  # 64-aligned, a zero tail
+    P = x.size
+    zero = torch.zeros(P, device="cuda")
+    out = torch.empty(P, device="cuda")
+    gpu.mix_seq_div(out, zero, [_dev(x)], [1.0], [float(2 * o)])
+    ref = np.float32(0.0) + (np.float32(1.0) * (x - np.float32(0.0))) / np.float32(2 * o)
+    got = out.cpu().numpy()
+    same = got.view(np.uint32) == ref.view(np.uint32)
+    assert same.all(), (o, x[~same][:4], got[~same][:4], ref[~same][:4])
+
+
 @pytest.mark.parametrize("divisors", [[float(c) for c in range(1, 33)], [3.0, 1e-6, 7e5, 0.1, 2.0 ** 20, 2.0 ** -20]])
 def test_fold_f64_div_quotient_exact_over_exponent_range(gpu, divisors):
     """fp64 divisor fold (cfa_fold_f64, SEQUENTIAL_DIV): with local = 0 and u = 1 the one-step
