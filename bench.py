@@ -85,9 +85,20 @@ def parse():
                    help="whole halo in one exchange step (boundary devices wait for all of it)")
     p.add_argument("--no-extra-legs", "--no-params-leg", dest="no_extra_legs", action="store_true",
                    help="N > 1: skip the other partitions' measurements (devices, hybrid2) beside the headline")
+    p.add_argument("--route-tune", default="links", choices=["links", "wallclock", "none"],
+                   help="N > 1: how the halo route is chosen. links (default): plan with per-link costs from "
+                        "the link probe's measured rates (the relayed plan is kept only where it shortens the "
+                        "predicted critical path); wallclock: round 4's autotune, the relayed plan against "
+                        "the direct-only plan over a few timed rounds each; none: uniform link costs")
     p.add_argument("--no-autotune", action="store_true",
-                   help="N > 1: time the relayed route as planned, without first comparing it with "
-                        "the direct-only route")
+                   help="N > 1: same as --route-tune none")
+    p.add_argument("--link-probe-mb", type=float, default=64.0,
+                   help="N > 1: message size (MB) of the per-link probe run before the route is planned "
+                        "(federated_amd/linkprobe.py; 0 = no probe)")
+    p.add_argument("--no-decomposition", action="store_true",
+                   help="N > 1: skip the exchange-only / compute-only sub-legs of the headline round")
+    p.add_argument("--decomp-steps", type=int, default=0,
+                   help="timed rounds of each decomposition sub-leg (0 = min(--steps, 10))")
     p.add_argument("--no-weak-leg", action="store_true",
                    help="N > 1: skip the weak-scaling reference leg (--devices devices per GPU)")
     p.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
@@ -306,6 +317,37 @@ def child_env(base: dict, t0: float, status_file: str) -> dict:
     env["PYTHONUNBUFFERED"] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool: dmabuf IPC only
     return env
+
+
+def setup_rccl_diagnostics(rank: int, environ=None):
+    """N > 1, before anything initialises RCCL: NCCL_DEBUG=WARN when unset, and RCCL's log in a
+    per-rank file when NCCL_DEBUG_FILE is unset, so that the text of RCCL's own warning can go into
+    the line when opening the communicator or a collective fails (``rccl_log_tail``). Returns the
+    log's path (None when the caller's NCCL_DEBUG_FILE has a %-pattern)."""
+    import tempfile
+    env = os.environ if environ is None else environ
+    env.setdefault("NCCL_DEBUG", "WARN")
+    if env.get("NCCL_DEBUG_FILE"):
+        path = env["NCCL_DEBUG_FILE"]
+        return None if "%" in path else path
+    path = os.path.join(tempfile.gettempdir(), f"cfa_rccl_r{rank}_{os.getpid()}.log")
+    env["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def rccl_log_tail(path, limit: int = 1500) -> str:
+    """The last ``limit`` bytes of RCCL's log (its warnings), or ''."""
+    if not path:
+        return ""
+    try:
+        with open(path, "rb") as fh:
+            fh.seek(0, 2)
+            n = fh.tell()
+            fh.seek(max(0, n - limit))
+            data = fh.read()
+    except OSError:
+        return ""
+    return data.decode("utf-8", "replace").strip()
 
 
 def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python: str = None) -> int:
@@ -695,6 +737,134 @@ def leg_slice_P(partition: str, groups, world: int, P: int) -> int:
     return P
 
 
+def decomposition_estimate(step_s: float, steps: int, warmup: int) -> float:
+    """Seconds the two decomposition sub-legs are expected to take: each at most a headline round
+    per round (the exchange alone and the mixes alone are each shorter than the overlapped
+    round), warm-up included, with a 1.5x margin and the barriers' few seconds."""
+    return 1.5 * 2.0 * step_s * (steps + warmup) + 5.0
+
+
+def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: float, rates=None,
+                    host_staged: bool = False) -> dict:
+    """The N > 1 headline round taken apart on the headline's own shard (round-4 review):
+
+    (a) exchange only: the routed halo with no mixes, ``steps`` rounds after ``warmup``, each group
+        bracketed by HIP events on the comm stream (host clock on a host-staged transport); per
+        group its time (median over rounds, max over ranks), the busiest link's bytes and the rate
+        that gives (GB/s per link direction), and the time the link probe's rates predict for it;
+    (b) compute only: every device's mix with the halo rows already landed, HIP events around each
+        round's mixes: t_mix per device, and delta = the headline's interior per-launch time (mixes
+        overlapped with the exchange) / t_mix - 1, the CU and HBM time RCCL's copies take;
+    (c) the model: ``predict_round_ms`` (exchange groups back to back, mixes stretched by 1 + delta
+        while the exchange runs, each boundary set after its group) and the simple bound
+        max(L t_mix (1 + delta), exchange + tail mixes), both max over ranks, next to the achieved
+        ms per round.
+    Collective over the default group. Returns the line's ``decomposition`` object."""
+    import torch
+    import torch.distributed as dist
+    from federated_amd.population import predict_round_ms
+
+    plan = shard._route_plan
+    routed = shard.routed()
+    G = len(plan.groups)
+    compute = torch.cuda.current_stream()
+    comm = torch.cuda.Stream()
+
+    def barrier():
+        torch.cuda.synchronize()
+        dist.barrier()
+
+    marks = []
+
+    def exchange_round(record: bool):
+        if not host_staged:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(G + 1)]
+            evs[0].record(comm)
+            routed.run(comm, group_done=lambda g: evs[g + 1].record(comm))
+        else:
+            torch.cuda.synchronize()
+            evs = [time.perf_counter()]
+
+            def done(g):
+                torch.cuda.synchronize()
+                evs.append(time.perf_counter())
+            routed.run(comm, group_done=done)
+        if record:
+            marks.append(evs)
+
+    comm.wait_stream(compute)
+    for _ in range(warmup):
+        exchange_round(False)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        exchange_round(True)
+    barrier()
+    x_el = time.perf_counter() - t0
+    if host_staged:
+        per = [[(m[g + 1] - m[g]) * 1e3 for g in range(G)] for m in marks]
+    else:
+        per = [[m[g].elapsed_time(m[g + 1]) for g in range(G)] for m in marks]
+    group_ms = [statistics.median(col) for col in zip(*per)] if G else []
+
+    L = shard.plan.L
+    evc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for _ in range(warmup):
+        shard.compute_round(compute)
+    barrier()
+    t0 = time.perf_counter()
+    for a, b in evc:
+        a.record(compute)
+        shard.compute_round(compute)
+        b.record(compute)
+    barrier()
+    c_el = time.perf_counter() - t0
+    t_mix = statistics.median(a.elapsed_time(b) for a, b in evc) / max(1, L)
+    delta = head_avg_ms / t_mix - 1.0 if (head_avg_ms and t_mix > 0) else 0.0
+
+    schedule = shard.boundary_schedule()
+    n_int = len(shard.interior_order())
+    sim = predict_round_ms(group_ms, schedule, n_int, t_mix, max(0.0, delta))
+    x_round = sum(group_ms)
+    tail_devices = sum(n for g, n in schedule if g >= G - 1)
+    compute_bound = L * t_mix * (1.0 + max(0.0, delta))
+    simple = max(compute_bound, x_round + tail_devices * t_mix)
+    # max over ranks of every figure (the round ends with the slowest rank)
+    vec = torch.tensor([x_el, c_el, t_mix, delta, sim, simple, compute_bound] + group_ms, dtype=torch.float64)
+    dist.all_reduce(vec, op=dist.ReduceOp.MAX)
+    x_el, c_el, t_mix, delta, sim, simple, compute_bound = vec[:7].tolist()
+    group_ms = vec[7:].tolist()
+    x_round = sum(group_ms)
+    pred = plan.predicted_group_ms(rates) if rates else [None] * G
+    groups = []
+    for g in range(G):
+        busiest = max(plan.group_link_elems(g).values(), default=0) * 4
+        groups.append({"ms": round(group_ms[g], 4), "busiest_link_MB": round(busiest / 1e6, 2),
+                       "link_GBps": round(busiest / (group_ms[g] * 1e-3) / 1e9, 2) if group_ms[g] > 0 else None,
+                       "predicted_ms": round(pred[g], 4) if pred[g] is not None else None})
+    crit = plan.critical_elems() * 4
+    return {
+        "steps": steps,
+        "exchange_only_ms": round(x_el / steps * 1e3, 4),
+        "exchange_groups_ms_sum": round(x_round, 4),
+        "exchange_link_GBps": round(crit / (x_round * 1e-3) / 1e9, 2) if x_round > 0 else None,
+        "exchange_predicted_ms": round(sum(pred), 4) if rates else None,
+        "exchange_groups": groups,
+        "compute_only_ms": round(c_el / steps * 1e3, 4),
+        "t_mix_ms": round(t_mix, 5),
+        "delta": round(delta, 4),
+        "interior_devices": n_int,
+        "tail_devices": tail_devices,
+        "tail_ms": round(tail_devices * t_mix, 4),
+        "compute_bound_ms": round(compute_bound, 4),
+        "model_prediction_ms": round(simple, 4),
+        "model_simulated_ms": round(sim, 4),
+        "bound": "exchange" if x_round + tail_devices * t_mix > compute_bound else "compute",
+        "timing": "host clock per group (host-staged transport)" if host_staged else
+                  "HIP events per exchange group on the comm stream; per-round mixes on the compute stream",
+    }
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -710,6 +880,8 @@ def main():
     if wd is None:
         wd = args.total_seconds + 90.0 if args.total_seconds > 0 else 900.0
     watchdog = Watchdog(wd, rank, t0)
+    rccl_log = setup_rccl_diagnostics(rank) if world > 1 else None  # before anything opens RCCL
+    route_tune = "none" if args.no_autotune else args.route_tune
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
     import torch
@@ -757,7 +929,10 @@ def main():
             tstate["transport"], tstate["comparable"] = open_transport(args.transport, rank, world, device,
                                                                        args.allow_fallback)
         except TransportError as exc:
-            tstate["error"] = str(exc)
+            tail = rccl_log_tail(rccl_log)
+            tstate["error"] = str(exc) + (f" [RCCL log: {tail}]" if tail else "")
+            if tail:
+                print(f"[bench rank {rank}] RCCL log tail:\n{tail}", file=sys.stderr, flush=True)
         return tstate["transport"]
 
     headline_fallback = None
@@ -775,6 +950,29 @@ def main():
         headline_fallback = {"wanted": headline, "measured": "params", "error": tstate["error"]}
         headline, headline_exchanges = "params", False
 
+    # Per-link rates of the node, measured over the headline's transport before any route is
+    # planned (federated_amd/linkprobe.py): with --route-tune links (default) they become the
+    # route plan's link costs, and every line at N > 1 reports them (config.links)
+    probe = {"result": None, "costs": None, "summary": None, "error": None}
+    if headline_exchanges and args.link_probe_mb > 0 and tstate["transport"] is not None:
+        watchdog.enter("link probe")
+        from federated_amd.halo import link_costs_from_rates
+        from federated_amd.linkprobe import probe_links, summarize
+        t_probe = time.perf_counter()
+        try:
+            res = probe_links(tstate["transport"], rank, world, device, elems=int(args.link_probe_mb * 1e6 / 4))
+            probe.update(result=res, summary=summarize(res, world))
+            if route_tune == "links":
+                probe["costs"] = link_costs_from_rates(res["rates"])
+        except Exception as exc:
+            tail = rccl_log_tail(rccl_log)
+            probe["error"] = f"{type(exc).__name__}: {exc}" + (f" [RCCL log: {tail}]" if tail else "")
+            print(f"[bench rank {rank}] link probe failed: {probe['error']}", file=sys.stderr, flush=True)
+        if not agree_all(probe["error"] is None):
+            probe.update(result=None, costs=None, summary=None, error=probe["error"] or "failed on another rank")
+        if probe["summary"] is not None:
+            probe["summary"]["wall_s"] = round(time.perf_counter() - t_probe, 2)
+
     def build(partition, devices=None, relay=None):
         transport = tstate["transport"]
         shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
@@ -783,7 +981,7 @@ def main():
                                       relay=(not args.no_relay) if relay is None else relay,
                                       staged=not args.no_stages, window_batch=args.window_batch,
                                       placement_candidates=args.placement_candidates,
-                                      placement_release=args.placement_release)
+                                      placement_release=args.placement_release, link_cost=probe["costs"])
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -799,20 +997,38 @@ def main():
         if args.placement_release:
             torch.cuda.empty_cache()
 
+    def route_choice(xshard):
+        """How the shard's route was chosen, for halo_route.autotune: with measured link costs the
+        plan itself keeps relays only where they shorten the predicted critical path; its predicted
+        exchange time at the probe's rates beside the direct-only plan's."""
+        plan = xshard._route_plan
+        out = {"mode": route_tune, "chosen": "relayed" if plan.relay else "direct",
+               "link_cost": "measured" if plan.link_cost else "uniform"}
+        rates = (probe["result"] or {}).get("rates")
+        if rates:
+            from federated_amd.halo import RoutePlan
+            direct = RoutePlan(world, plan.transfers, relay=False, link_cost=plan.link_cost)
+            out["predicted_ms"] = round(plan.predicted_ms(rates), 4)
+            out["direct_predicted_ms"] = round(direct.predicted_ms(rates), 4)
+        return out
+
     def build_tuned(partition, devices=None):
-        """The shard of ``partition``; with a relayed route at N > 1, route autotune before any timed
-        region: the relayed plan against the direct-only plan, a few rounds each after warm-up, max
-        over ranks; the faster one is kept (the cost model assumes every link runs at the same
-        rate; this checks it on the node). Returns (shard, info, autotune or None)."""
+        """The shard of ``partition`` and how its route was chosen (N > 1): from the link probe's
+        measured rates (--route-tune links, default; the plan keeps relays only where they shorten
+        the predicted critical path), or round 4's wall-clock autotune (--route-tune wallclock: the
+        relayed plan against the direct-only plan, a few rounds each after warm-up, max over
+        ranks; the faster one is kept). Returns (shard, info, route choice or None)."""
         xshard, xinfo = build(partition, devices)
-        if not (world > 1 and xinfo.get("route", {}).get("relay") and not args.no_autotune):
+        if not (world > 1 and xinfo.get("route")):
             return xshard, xinfo, None
+        if route_tune != "wallclock" or not xinfo["route"].get("relay"):
+            return xshard, xinfo, route_choice(xshard)
         tune_steps = 3
         watchdog.enter(f"route autotune ({partition})")
         t_rel, _, _ = run_leg(args, xshard, world, tune_steps, args.warmup, timed_kernel=False)
         dshard, dinfo = build(partition, devices, relay=False)
         t_dir, _, _ = run_leg(args, dshard, world, tune_steps, args.warmup, timed_kernel=False)
-        tune = {"relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
+        tune = {"mode": "wallclock", "relayed_ms_per_step": round(t_rel / tune_steps * 1e3, 4),
                 "direct_ms_per_step": round(t_dir / tune_steps * 1e3, 4)}
         # same decision on every rank: both times are maxima over ranks. The losing plan's stacks
         # stay in torch's cache: memory returned to the driver is scrubbed in the background, which
@@ -854,6 +1070,9 @@ def main():
             res = measure_headline(headline)
         except Exception as exc:
             err = f"{type(exc).__name__}: {exc}"
+            tail = rccl_log_tail(rccl_log)
+            if tail:
+                err += f" [RCCL log: {tail}]"
             print(f"[bench rank {rank}] {headline} headline failed: {err}", file=sys.stderr, flush=True)
         if not agree_all(err is None):
             if headline == "params":
@@ -877,6 +1096,28 @@ def main():
         watchdog.enter("timed rounds, scattered order")
         scat = timed_scattered(shard, args.steps)
     t_headline = time.perf_counter() - t_head0
+
+    # N > 1: the headline round taken apart on the headline's own shard (exchange only, compute
+    # only, the model's prediction), so a scaling result explains itself; budget-gated (the
+    # headline never is)
+    decomp = None
+    if world > 1 and headline_exchanges and route is not None and not args.no_decomposition:
+        dsteps = args.decomp_steps or min(args.steps, 10)
+        est = decomposition_estimate(elapsed / args.steps, dsteps, args.warmup)
+        if agree_all(budget.left() - 15.0 >= est):
+            watchdog.enter("decomposition (exchange only, compute only)")
+            try:
+                decomp = decompose_round(shard, world, dsteps, args.warmup, avg_ms,
+                                         (probe["result"] or {}).get("rates"),
+                                         bool(getattr(tstate["transport"], "host_staged", False)))
+                decomp["achieved_ms"] = round(elapsed / args.steps * 1e3, 4)
+            except Exception as exc:
+                decomp = {"error": f"{type(exc).__name__}: {exc}"}
+                print(f"[bench rank {rank}] decomposition failed: {decomp['error']}", file=sys.stderr, flush=True)
+            if not agree_all("error" not in decomp):
+                decomp = {"error": decomp.get("error", "failed on another rank")}
+        else:
+            decomp = {"skipped": "budget", "estimate_s": round(est, 1), "budget_left_s": round(budget.left(), 1)}
 
     result = None
     if rank == 0:
@@ -916,10 +1157,14 @@ def main():
                 "transport": tstate["transport"].name if headline_exchanges else "none (no exchange)",
                 "comparable": tstate["comparable"] if headline_exchanges else True,
                 "halo_route": ({k: route[k] for k in ("relay", "stages", "groups", "messages",
-                                                     "max_messages_per_rank_group")}
+                                                     "max_messages_per_rank_group", "link_cost")}
                                | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
                                   "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
-                                  "autotune": autotune}) if route else None,
+                                  "autotune": autotune,
+                                  "predicted_critical_ms": (autotune or {}).get("predicted_ms"),
+                                  "achieved_critical_ms": (decomp or {}).get("exchange_groups_ms_sum")})
+                if route else None,
+                "links": probe["summary"] if probe["error"] is None else {"error": probe["error"]},
                 "placement": info.get("placement"),
                 "halo_carved": info.get("halo_carved"),
                 "cache_reuse": reuse,
@@ -960,6 +1205,8 @@ def main():
                     shard_P(info, P), K, kernel, args.window_batch or 1),
             },
         }
+        if decomp is not None:
+            result["decomposition"] = decomp
         if scat is not None:
             xel, xdur = scat
             result["value_scattered"] = round(bytes_total / xel / 1e9, 2)

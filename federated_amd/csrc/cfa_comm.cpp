@@ -24,7 +24,7 @@ extern "C" void cfa_internal_set_error(const char* msg);
 
 static int comm_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 static int comm_fail(int code, const char* fmt, ...) {
-  char buf[512];
+  char buf[1024];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
@@ -33,11 +33,19 @@ static int comm_fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// RCCL's own text for the last failure (ncclGetLastError: the warning it logged, e.g. which
+// transport or IPC call refused), so a failure on a node this build never ran on says why.
+static const char* rccl_detail() {
+  const char* d = ncclGetLastError(nullptr);
+  return d ? d : "";
+}
+
 #define CFA_NCCL_CHECK(expr)                                                               \
   do {                                                                                     \
     ncclResult_t r_ = (expr);                                                              \
     if (r_ != ncclSuccess)                                                                 \
-      return comm_fail(CFA_E_RCCL, "%s failed: %s", #expr, ncclGetErrorString(r_));        \
+      return comm_fail(CFA_E_RCCL, "%s failed: %s [rccl: %s]", #expr, ncclGetErrorString(r_), \
+                       rccl_detail());                                                      \
   } while (0)
 
 static_assert(sizeof(ncclUniqueId) == CFA_UNIQUE_ID_BYTES, "unique id size");
@@ -92,14 +100,16 @@ extern "C" int cfa_halo_exchange_f32(void* comm, const float* const* send_bufs,
     ncclResult_t r = ncclSend(send_bufs[i], P, ncclFloat32, send_peers[i], c, st);
     if (r != ncclSuccess) {
       ncclGroupEnd();
-      return comm_fail(CFA_E_RCCL, "ncclSend to %d: %s", send_peers[i], ncclGetErrorString(r));
+      return comm_fail(CFA_E_RCCL, "ncclSend to %d: %s [rccl: %s]", send_peers[i], ncclGetErrorString(r),
+                       rccl_detail());
     }
   }
   for (int i = 0; i < nrecv; ++i) {
     ncclResult_t r = ncclRecv(recv_bufs[i], P, ncclFloat32, recv_peers[i], c, st);
     if (r != ncclSuccess) {
       ncclGroupEnd();
-      return comm_fail(CFA_E_RCCL, "ncclRecv from %d: %s", recv_peers[i], ncclGetErrorString(r));
+      return comm_fail(CFA_E_RCCL, "ncclRecv from %d: %s [rccl: %s]", recv_peers[i], ncclGetErrorString(r),
+                       rccl_detail());
     }
   }
   CFA_NCCL_CHECK(ncclGroupEnd());
@@ -132,7 +142,8 @@ extern "C" int cfa_p2p_group_f32(void* comm, const float* const* send_bufs, cons
     ncclResult_t r = ncclSend(send_bufs[i], send_counts[i], ncclFloat32, send_peers[i], c, st);
     if (r != ncclSuccess) {
       ncclGroupEnd();
-      return comm_fail(CFA_E_RCCL, "ncclSend to %d: %s", send_peers[i], ncclGetErrorString(r));
+      return comm_fail(CFA_E_RCCL, "ncclSend to %d: %s [rccl: %s]", send_peers[i], ncclGetErrorString(r),
+                       rccl_detail());
     }
   }
   for (int i = 0; i < nrecv; ++i) {
@@ -140,7 +151,8 @@ extern "C" int cfa_p2p_group_f32(void* comm, const float* const* send_bufs, cons
     ncclResult_t r = ncclRecv(recv_bufs[i], recv_counts[i], ncclFloat32, recv_peers[i], c, st);
     if (r != ncclSuccess) {
       ncclGroupEnd();
-      return comm_fail(CFA_E_RCCL, "ncclRecv from %d: %s", recv_peers[i], ncclGetErrorString(r));
+      return comm_fail(CFA_E_RCCL, "ncclRecv from %d: %s [rccl: %s]", recv_peers[i], ncclGetErrorString(r),
+                       rccl_detail());
     }
   }
   CFA_NCCL_CHECK(ncclGroupEnd());

@@ -25,6 +25,11 @@ This module spreads the halo over every link:
   stage g - 1, so groups run back to back on one stream and every link stays busy. Stage s is
   complete after group s + 1 (after group s when nothing is relayed). A relay rank keeps the
   pieces in two staging slots, by stage parity.
+* **Measured links** (``link_cost``). By default every link costs the same per element. Given
+  integer costs per directed link (``link_costs_from_rates`` of the rates ``linkprobe`` measures
+  on the node), a part's weight on a link is its elements times that link's cost, so the greedy
+  moves parts off slow links and the critical path is in time units; ``predicted_ms`` turns a
+  plan back into milliseconds with the measured rates.
 * **Messages.** Each piece is one contiguous element range, so a message is one RCCL
   send/recv of a plain buffer slice. Within a group, every rank lists its sends to a peer in the
   order of one global message list, and the peer lists its receives in that same order, so the
@@ -76,7 +81,8 @@ def relay_key(parity: int) -> tuple:
 
 
 def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int = 64,
-                 relay: bool = True) -> Tuple[Dict[Tuple[int, int, int], List[Tuple[int, int]]], Dict]:
+                 relay: bool = True, cost: Optional[Dict[Tuple[int, int], int]] = None
+                 ) -> Tuple[Dict[Tuple[int, int, int], List[Tuple[int, int]]], Dict]:
     """Split every (group, a, b) demand over the direct link and 2-hop relays.
 
     ``demand[(g, a, b)]`` is the weight (elements) rank a sends rank b in stage position g. A
@@ -85,9 +91,12 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
     the exchange's critical path (the sum over groups of the busiest link's load, groups running
     back to back), then to the path whose busiest link ends up least loaded, then to fewer hops,
     then to the lower relay rank: integer arithmetic with a fixed order, so every rank computes
-    the same routes. Returns ``shares[(g, a, b)]`` = [(path, n_units)], path = DIRECT or the
-    relay rank, direct first then relays ascending, n_units summing to ``units``; and the link
-    loads per group, ``{(g, a, b): weight}``."""
+    the same routes. ``cost[(a, b)]`` (positive integers, default 1 for every link) scales a
+    part's weight on link a->b: with costs proportional to 1 / measured rate the loads are times.
+    Returns ``shares[(g, a, b)]`` = [(path, n_units)], path = DIRECT or the relay rank, direct
+    first then relays ascending, n_units summing to ``units``; and the link loads per group,
+    ``{(g, a, b): weight}``."""
+    c = (lambda a, b: 1) if not cost else (lambda a, b: int(cost.get((a, b), 1)))
     load: Dict[Tuple[int, int, int], int] = defaultdict(int)
     gmax: Dict[int, int] = defaultdict(int)
     counts = {key: defaultdict(int) for key in demand}
@@ -102,12 +111,12 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
                 cands = [DIRECT] + ([k for k in range(world) if k != a and k != b] if relay else [])
                 for k in cands:
                     links = [(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]
-                    delta = sum(max(0, load[l] + w - gmax[l[0]]) for l in links)
-                    cost = (delta, max(load[l] + w for l in links), len(links), k)
-                    if best_cost is None or cost < best_cost:
-                        best, best_cost = k, cost
+                    delta = sum(max(0, load[l] + w * c(l[1], l[2]) - gmax[l[0]]) for l in links)
+                    key_cost = (delta, max(load[l] + w * c(l[1], l[2]) for l in links), len(links), k)
+                    if best_cost is None or key_cost < best_cost:
+                        best, best_cost = k, key_cost
                 for l in ([(g, a, b)] if best == DIRECT else [(g, a, best), (g + 1, best, b)]):
-                    load[l] += w
+                    load[l] += w * c(l[1], l[2])
                     gmax[l[0]] = max(gmax[l[0]], load[l])
                 counts[key][best] += 1
     shares = {}
@@ -118,15 +127,15 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
     return shares, dict(load)
 
 
-def _critical(shares, demand) -> int:
-    """Sum over groups of the busiest link's weight for a set of shares."""
+def _critical(shares, demand, cost=None) -> int:
+    """Sum over groups of the busiest link's (cost-weighted) load for a set of shares."""
     load: Dict[Tuple[int, int, int], int] = defaultdict(int)
     for (g, a, b), parts in shares.items():
         units = sum(n for _, n in parts) or 1
         for k, n in parts:
             w = demand[(g, a, b)] * n // units
             for l in ([(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]):
-                load[l] += w
+                load[l] += w * (int(cost.get((l[1], l[2]), 1)) if cost else 1)
     gmax: Dict[int, int] = defaultdict(int)
     for (g, _, _), w in load.items():
         gmax[g] = max(gmax[g], w)
@@ -148,8 +157,15 @@ class RoutePlan:
     """The global message schedule of one routed exchange (identical on every rank)."""
 
     def __init__(self, world: int, transfers: Sequence[Transfer], relay: bool = True, units: int = 64,
-                 align: int = ALIGN):
+                 align: int = ALIGN, link_cost: Optional[Dict[Tuple[int, int], int]] = None):
+        """``link_cost``: integer cost per element of each directed link (``link_costs_from_rates``);
+        None = every link alike. Every rank must pass the same costs (the digest covers the
+        routes they produce)."""
         self.world = int(world)
+        self.link_cost = {k: int(v) for k, v in link_cost.items()} if link_cost else None
+        for k, v in (self.link_cost or {}).items():
+            if v < 1:
+                raise ValueError(f"link cost must be a positive integer, got {k}: {v}")
         self.transfers = list(transfers)
         self.units, self.align = int(units), int(align)
         for t in self.transfers:
@@ -161,10 +177,12 @@ class RoutePlan:
         for t in self.transfers:
             demand[(self._stage_pos[t.stage], t.src, t.dst)] += t.hi - t.lo
         self.relay = bool(relay) and world >= 3
-        self.shares, _ = route_shares(world, dict(demand), self.units, self.relay)
-        if self.relay:  # keep relays only where they shorten the critical path
-            direct, _ = route_shares(world, dict(demand), self.units, False)
-            if _critical(direct, dict(demand)) <= _critical(self.shares, dict(demand)):
+        lc = self.link_cost
+        self.shares, _ = route_shares(world, dict(demand), self.units, self.relay, lc)
+        self.relay_considered = self.relay
+        if self.relay:  # keep relays only where they shorten the (cost-weighted) critical path
+            direct, _ = route_shares(world, dict(demand), self.units, False, lc)
+            if _critical(direct, dict(demand), lc) <= _critical(self.shares, dict(demand), lc):
                 self.relay, self.shares = False, direct
         self.groups: List[List[Message]] = [[] for _ in range(len(self.stages) + (1 if self.relay else 0))]
         slot_use = defaultdict(int)  # (rank, stage) -> relay elements
@@ -228,6 +246,34 @@ class RoutePlan:
         elements per link-second when groups run back to back."""
         return sum(max(self.group_link_elems(g).values(), default=0) for g in range(len(self.groups)))
 
+    def critical_cost(self) -> int:
+        """Sum over groups of the busiest link's elements times that link's cost (= critical_elems
+        when every link costs the same)."""
+        total = 0
+        for g in range(len(self.groups)):
+            load = self.group_link_elems(g)
+            total += max((n * (self.link_cost.get(l, 1) if self.link_cost else 1) for l, n in load.items()),
+                         default=0)
+        return total
+
+    def predicted_group_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4) -> List[float]:
+        """Per group, the time its slowest link needs at the given per-direction rates (GB/s; a link
+        missing from ``rates_gbps`` takes the slowest rate given): the group's length when every
+        link runs at its measured rate and the groups run back to back."""
+        slow = min(rates_gbps.values()) if rates_gbps else None
+        out = []
+        for g in range(len(self.groups)):
+            t = 0.0
+            for l, n in self.group_link_elems(g).items():
+                r = rates_gbps.get(l, slow)
+                if r:
+                    t = max(t, n * elem_bytes / (r * 1e9) * 1e3)
+            out.append(t)
+        return out
+
+    def predicted_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4) -> float:
+        return sum(self.predicted_group_ms(rates_gbps, elem_bytes))
+
     def digest(self) -> str:
         h = hashlib.sha1()
         for g in self.groups:
@@ -245,6 +291,7 @@ class RoutePlan:
                  [self.rank_ops(x, g) for x in range(self.world)]), default=0),
             "max_link_elems": self.max_link_elems(),
             "critical_elems": self.critical_elems(),
+            "link_cost": "measured" if self.link_cost else "uniform",
         }
 
 
@@ -283,15 +330,37 @@ class RoutedExchange:
             self.ops.append(prep(s, r) if prep is not None else (s, r))
         self.done = [plan.stages_done_after(g) for g in range(len(plan.groups))]
 
-    def run(self, stream=None, stage_done: Optional[Callable[[int], None]] = None) -> None:
+    def run(self, stream=None, stage_done: Optional[Callable[[int], None]] = None,
+            group_done: Optional[Callable[[int], None]] = None) -> None:
+        """Issue every group in order; ``group_done(g)`` (optional) right after group g is issued
+        (the bench's exchange-only timing records an event there)."""
         for g, op in enumerate(self.ops):
             if callable(op):
                 op(stream)
             else:
                 self.transport.exchange(op[0], op[1], stream)
+            if group_done is not None:
+                group_done(g)
             if stage_done is not None:
                 for s in self.done[g]:
                     stage_done(s)
+
+
+def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int = 16) -> Dict[Tuple[int, int], int]:
+    """Integer per-element cost of each directed link from measured rates: the fastest link costs
+    ``scale``, a link at half its rate 2 * scale (rounded; at least 1). Integer so that every rank
+    plans the same routes from the same (all-reduced) rates."""
+    if not rates_gbps:
+        return {}
+    fastest = max(rates_gbps.values())
+    if not fastest > 0:
+        raise ValueError("link rates must be positive")
+    out = {}
+    for l, r in sorted(rates_gbps.items()):
+        if not r > 0:
+            raise ValueError(f"link {l} has no positive rate ({r})")
+        out[l] = max(1, int(round(scale * fastest / r)))
+    return out
 
 
 def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world: int = 1,

@@ -1,0 +1,170 @@
+"""Per-link rates of the node the population is sharded over, measured before the routed halo is planned.
+
+The reference has no collective (its neighbour models travel as files, TF1 ``cfa.py:119-130``);
+the sharded population's only exchange is the ring halo of ``halo.py``, whose route plan needs a
+cost per directed link. On one MI355X node every GPU has a direct xGMI link to each of the other
+seven, but their rates are not given (the design's cost model assumed 50-64 GB/s per direction,
+DESIGN.md §5): this module measures them with the same transport and message path the halo uses.
+
+* ``matching_rounds``: a 1-factorisation of the ranks (round-robin "circle" schedule), so in each
+  round every rank exchanges with exactly one partner and every link of the node is busy in both
+  directions once over the rounds, while no GPU drives two links at a time.
+* ``probe_links``: per round, each pair exchanges one ``elems``-float message each way, ``reps``
+  times after a warm-up, timed with HIP events on the exchange stream (host clock on a
+  host-staged transport); the pair's time is the slower end's. Then an all-peers pass: every rank
+  sends to and receives from all peers at once (equal chunks), the per-GPU egress rate with every
+  link busy together, which says whether the links of one GPU are independent (what the relayed
+  routes assume).
+
+Host logic (``matching_rounds``, ``rates_from_times``) is pure; ``probe_links`` runs on CPU tensors
+over gloo as well (tests), and on the GPU over RCCL or torch.distributed (bench.py).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Tuple
+
+ALIGN = 64
+
+
+def matching_rounds(world: int) -> List[List[Tuple[int, int]]]:
+    """Rounds of disjoint rank pairs covering every unordered pair exactly once (world - 1 rounds
+    for an even world, world rounds with one rank idle per round for an odd one)."""
+    if world < 2:
+        return []
+    n = world + (world % 2)
+    ring = list(range(n))
+    rounds = []
+    for _ in range(n - 1):
+        pairs = []
+        for i in range(n // 2):
+            a, b = ring[i], ring[n - 1 - i]
+            if a < world and b < world:
+                pairs.append((min(a, b), max(a, b)))
+        rounds.append(sorted(pairs))
+        ring = [ring[0], ring[-1]] + ring[1:-1]
+    return rounds
+
+
+def rates_from_times(times_s, elems: int, elem_bytes: int = 4) -> Dict[Tuple[int, int], float]:
+    """Per-direction GB/s of every directed link from a [world][world] matrix of exchange times
+    (seconds; entry [a][b] measured on rank a for its exchange with b, 0 = not measured): link a->b
+    and b->a both take the slower end's time of their (bidirectional) exchange."""
+    world = len(times_s)
+    out = {}
+    for a in range(world):
+        for b in range(world):
+            if a == b:
+                continue
+            t = max(float(times_s[a][b]), float(times_s[b][a]))
+            if t > 0:
+                out[(a, b)] = elems * elem_bytes / t / 1e9
+    return out
+
+
+def _prepare(transport, sends, recvs):
+    prep = getattr(transport, "prepare", None)
+    if prep is not None:
+        return prep(sends, recvs)
+    return lambda stream=None: transport.exchange(sends, recvs, stream)
+
+
+def _timed(op, stream, reps: int, warmup: int, device_timing: bool) -> float:
+    """Seconds per call of ``op(stream)``: HIP events around ``reps`` back-to-back calls on the
+    stream (device transports), else the host clock with the stream drained on both sides."""
+    import torch
+    for _ in range(warmup):
+        op(stream)
+    if stream is not None:
+        stream.synchronize()
+    if device_timing:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            op(stream)
+        b.record(stream)
+        b.synchronize()
+        return a.elapsed_time(b) / 1e3 / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        op(stream)
+    if stream is not None:
+        stream.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def probe_links(transport, rank: int, world: int, device=None, elems: int = 16 << 20, reps: int = 3,
+                warmup: int = 1, all_peers: bool = True, group=None) -> dict:
+    """Measure every directed link (see the module docstring). Collective over the default
+    torch.distributed group (``group``: another control group): every rank calls it with the same
+    arguments. Returns {"rates": {(a, b): GB/s}, "pair_ms": [[ms]], "elems": elems,
+    "all_peers": {"egress_GBps": [per rank], "chunk_elems": c} or None} identical on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    elems = max(ALIGN, elems // ALIGN * ALIGN)
+    send = torch.full((elems,), float(rank), dtype=torch.float32, device=dev)
+    recv = torch.empty(elems, dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+    device_timing = dev.type == "cuda" and not getattr(transport, "host_staged", False)
+    times = torch.zeros((world, world), dtype=torch.float64)
+    for pairs in matching_rounds(world):
+        dist.barrier(group=group)  # one round at a time: no GPU drives two links
+        partner = next((b if a == rank else a for a, b in pairs if rank in (a, b)), None)
+        if partner is None:
+            continue
+        op = _prepare(transport, [(send, partner)], [(recv, partner)])
+        times[rank, partner] = _timed(op, stream, reps, warmup, device_timing)
+        if float(recv[0].item()) != float(partner):
+            raise RuntimeError(f"link probe: rank {rank} received {float(recv[0].item())} from {partner}")
+    dist.all_reduce(times, op=dist.ReduceOp.SUM, group=group)  # each entry written by one rank
+    res = {"elems": elems, "rates": rates_from_times(times.tolist(), elems),
+           "pair_ms": [[round(float(t) * 1e3, 4) for t in row] for row in times.tolist()], "all_peers": None}
+    if all_peers and world > 2:
+        chunk = max(ALIGN, elems // (world - 1) // ALIGN * ALIGN)
+        peers = [p for p in range(world) if p != rank]
+        sends = [(send[i * chunk:(i + 1) * chunk], p) for i, p in enumerate(peers)]
+        recvs = [(recv[i * chunk:(i + 1) * chunk], p) for i, p in enumerate(peers)]
+        dist.barrier(group=group)
+        t = _timed(_prepare(transport, sends, recvs), stream, reps, warmup, device_timing)
+        for i, p in enumerate(peers):
+            if float(recv[i * chunk].item()) != float(p):
+                raise RuntimeError(f"link probe (all peers): rank {rank} chunk {i} not from {p}")
+        tv = torch.zeros(world, dtype=torch.float64)
+        tv[rank] = t
+        dist.all_reduce(tv, op=dist.ReduceOp.SUM, group=group)
+        res["all_peers"] = {"chunk_elems": chunk,
+                            "egress_GBps": [round((world - 1) * chunk * 4 / float(x) / 1e9, 2) if x > 0 else None
+                                            for x in tv.tolist()]}
+    del send, recv
+    return res
+
+
+def summarize(probe: dict, world: int) -> dict:
+    """The bench line's view of a probe: the rate matrix (GB/s per direction, None on the
+    diagonal), its min / median / max, and the all-peers egress against the sum of one GPU's
+    pairwise link rates (1.0 = the links of a GPU add up; what relayed routes assume)."""
+    import statistics
+    rates = probe["rates"]
+    mat = [[round(rates[(a, b)], 2) if (a, b) in rates else None for b in range(world)] for a in range(world)]
+    vals = sorted(rates.values())
+    out = {"message_MB": round(probe["elems"] * 4 / 1e6, 1), "rates_GBps": mat,
+           "min_GBps": round(vals[0], 2) if vals else None,
+           "median_GBps": round(statistics.median(vals), 2) if vals else None,
+           "max_GBps": round(vals[-1], 2) if vals else None}
+    ap = probe.get("all_peers")
+    if ap:
+        eg = ap["egress_GBps"]
+        sums = [sum(rates.get((a, b), 0.0) for b in range(world) if b != a) for a in range(world)]
+        out["all_peers_egress_GBps"] = eg
+        out["all_peers_vs_link_sum"] = [round(e / s, 3) if (e and s) else None for e, s in zip(eg, sums)]
+    return out
+
+
+def min_rate(probe: Optional[dict]) -> Optional[float]:
+    if not probe or not probe.get("rates"):
+        return None
+    return min(probe["rates"].values())

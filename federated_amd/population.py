@@ -320,6 +320,21 @@ class RingPopulationShard:
             if timer:
                 timer(i, False)
 
+    def compute_round(self, stream=None, timer=None) -> None:
+        """Every device's mix and nothing else (the halo rows hold what the last exchange
+        delivered): the compute-only round of the bench's N > 1 decomposition. ``timer`` as in
+        ``round``, around every mix."""
+        cs = stream or torch.cuda.current_stream(self.device)
+        self._mix_set(self.interior_order() + self.plan.boundary(), cs, timer)
+
+    def boundary_schedule(self) -> List[Tuple[int, int]]:
+        """[(exchange group after which they can mix, number of boundary devices)], in the order a
+        round mixes them (host logic; ``predict_round_ms``'s input)."""
+        route = self._route_plan
+        if route is None:
+            return []
+        return [(route.done_group(stage), len(devs)) for stage, devs in self.stage_sets()]
+
     def stage_sets(self) -> List[Tuple[int, List[int]]]:
         """[(stage, boundary devices that can mix once that stage has landed)], stage order."""
         by = {}
@@ -368,11 +383,39 @@ class RingPopulationShard:
         return self.plan.L * (self.plan.K + 2) * self.P * self.models.element_size()
 
 
+def predict_round_ms(group_ms: List[float], schedule: List[Tuple[int, int]], n_interior: int, t_mix_ms: float,
+                     delta: float) -> float:
+    """Length of one overlapped round from its measured parts (the bench's N > 1 decomposition):
+    the exchange groups run back to back from t = 0 on the comm stream (``group_ms``, measured
+    with no mixes); the compute stream mixes the ``n_interior`` interior devices from t = 0, then
+    each boundary set of ``schedule`` [(group, devices)] once its group has landed. A mix takes
+    ``t_mix_ms`` (measured with no exchange) stretched by (1 + ``delta``) while the exchange is
+    still running (RCCL's copy kernels share the CUs and HBM; ``delta`` measured from the
+    headline's own interior mixes), ``t_mix_ms`` after it."""
+    ends, t = [], 0.0
+    for g in group_ms:
+        t += g
+        ends.append(t)
+    t_x = ends[-1] if ends else 0.0
+
+    def mixes(n, t):
+        for _ in range(n):
+            t += t_mix_ms * (1.0 + delta) if t < t_x else t_mix_ms
+        return t
+
+    t = mixes(n_interior, 0.0)
+    for g, n in schedule:
+        if ends:
+            t = max(t, ends[min(g, len(ends) - 1)])
+        t = mixes(n, t)
+    return max(t, t_x)
+
+
 def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: int, device,
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
                     window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
-                    placement_release: bool = False):
+                    placement_release: bool = False, link_cost=None):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -382,7 +425,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     row so boundary devices mix as their rows land (both only matter when Gd > 1).
     ``placement_candidates`` > 1 allocates the shard's stacks placement-calibrated
     (``placement.calibrated_stacks``: the fastest of that many allocations each, timed with the
-    shard's own mix; ``info["placement"]`` holds the probe)."""
+    shard's own mix; ``info["placement"]`` holds the probe). ``link_cost``: measured per-link costs
+    for the route plan (``halo.link_costs_from_rates``; None = every link alike)."""
     from .halo import RoutePlan, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
@@ -394,7 +438,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
-        route = RoutePlan(world, tr, relay=relay)
+        route = RoutePlan(world, tr, relay=relay, link_cost=link_cost)
     Pr = bounds[p + 1] - bounds[p]
     stacks, placement = None, None
     if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":

@@ -32,4 +32,5 @@ ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataT
 ncclResult_t ncclReduce(const void* send, void* recv, size_t count, ncclDataType_t type, ncclRedOp_t op,
                         int root, ncclComm_t comm, hipStream_t stream);
 const char* ncclGetErrorString(ncclResult_t r);
+const char* ncclGetLastError(ncclComm_t comm);
 }

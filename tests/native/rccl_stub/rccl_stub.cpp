@@ -106,6 +106,7 @@ ncclResult_t ncclReduce(const void* send, void* recv, size_t count, ncclDataType
   return ncclSuccess;
 }
 const char* ncclGetErrorString(ncclResult_t r) { return r == ncclSuccess ? "ncclSuccess" : "ncclInvalidArgument"; }
+const char* ncclGetLastError(ncclComm_t) { return "stub: peer refused"; }
 
 // libcfa's error hook (cfa_mix.hip in the real library)
 void cfa_internal_set_error(const char* msg) { last_error = msg ? msg : ""; }

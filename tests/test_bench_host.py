@@ -263,3 +263,42 @@ def test_self_launch_forwards_a_termination_to_the_ranks(tmp_path):
     _t.sleep(0.2)
     with pytest.raises(ProcessLookupError):
         os.kill(child, 0)
+
+
+def test_rccl_diagnostics_only_fill_what_is_unset(tmp_path):
+    """N > 1 ranks get NCCL_DEBUG=WARN and a per-rank RCCL log file unless the caller set them;
+    the tail of that log is what goes into headline_fallback.error / links.error on a failure."""
+    import bench
+    env = {}
+    path = bench.setup_rccl_diagnostics(3, env)
+    assert env["NCCL_DEBUG"] == "WARN" and env["NCCL_DEBUG_FILE"] == path and "_r3_" in path
+    env = {"NCCL_DEBUG": "INFO", "NCCL_DEBUG_FILE": str(tmp_path / "mine.log")}
+    assert bench.setup_rccl_diagnostics(0, env) == str(tmp_path / "mine.log") and env["NCCL_DEBUG"] == "INFO"
+    assert bench.setup_rccl_diagnostics(0, {"NCCL_DEBUG_FILE": "/tmp/x.%h.%p"}) is None
+    log = tmp_path / "rccl.log"
+    log.write_text("x" * 5000 + "\nnode:1:1 [0] NCCL WARN Cuda failure 'invalid device ordinal'\n")
+    tail = bench.rccl_log_tail(str(log), limit=200)
+    assert tail.endswith("invalid device ordinal'") and len(tail) <= 200
+    assert bench.rccl_log_tail(str(tmp_path / "missing")) == "" and bench.rccl_log_tail(None) == ""
+
+
+def test_decomposition_is_budget_gated_and_never_the_headline():
+    """The decomposition sub-legs (exchange only, compute only) run only when the budget left covers
+    their estimate; the estimate scales with the headline's own round time."""
+    import bench
+    est = bench.decomposition_estimate(0.010, 10, 3)
+    assert est == pytest.approx(1.5 * 2 * 0.010 * 13 + 5.0)
+    assert bench.decomposition_estimate(0.1, 10, 3) > est
+    b = bench.Budget(420, t0=0.0, clock=lambda: 410.0)
+    assert not b.allows(15.0 + est)  # 10 s left: dropped, reported as skipped: budget
+    assert bench.Budget(420, t0=0.0, clock=lambda: 10.0).allows(15.0 + est)
+
+
+def test_bench_parses_the_route_and_decomposition_flags(monkeypatch):
+    import bench
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    a = bench.parse()
+    assert a.route_tune == "links" and a.link_probe_mb == 64.0 and not a.no_decomposition and a.decomp_steps == 0
+    monkeypatch.setattr("sys.argv", ["bench.py", "--route-tune", "wallclock", "--no-decomposition"])
+    a = bench.parse()
+    assert a.route_tune == "wallclock" and a.no_decomposition

@@ -205,3 +205,15 @@ def test_halo_exchange_and_collectives_forward_to_rccl(stub):
     assert lines == ["start", f"send 2 16 {a.data_ptr()} 7", f"recv 0 16 {b.data_ptr()} 7", "end",
                      f"allreduce 16 {a.data_ptr()} {a.data_ptr()}", f"reduce 3 16 {a.data_ptr()} {b.data_ptr()}"]
     assert np.all(a.numpy() == 0)
+
+
+def test_rccl_failure_carries_rccl_text(stub):
+    """An RCCL call that fails returns CFA_E_RCCL with ncclGetErrorString AND RCCL's own last
+    warning (ncclGetLastError), so a bench line's headline_fallback.error says why (round-4 review).
+    cfa_halo_exchange_f32 does not pre-validate peers: the stub's ncclSend refuses peer 9."""
+    t = stub_transport(stub, 0, 2)
+    a = torch.zeros(8)
+    L = t._lib
+    with pytest.raises(_lib.CFAError, match=r"ncclSend to 9: ncclInvalidArgument \[rccl: stub: peer refused\]"):
+        L.call("cfa_halo_exchange_f32", t.comm, L.ptr_table([a.data_ptr()]), L.int_array([9]), 1,
+               L.ptr_table([]), L.int_array([]), 0, 8, 7)

@@ -70,7 +70,23 @@ def test_self_launched_n2_line_matches_the_documented_schema():
         assert key in c, key
     assert c["partition"] == "devices" and c["headline_fallback"] is None
     assert c["transport"] == "torch-gloo" and c["comparable"] is False
-    assert set(c["halo_route"]) >= {"relay", "stages", "critical_MB", "autotune"}
+    assert set(c["halo_route"]) >= {"relay", "stages", "critical_MB", "autotune", "predicted_critical_ms",
+                                    "achieved_critical_ms", "link_cost"}
+    # round 5: the link probe's measured rates feed the route plan, and the round is decomposed
+    links = c["links"]
+    assert links["rates_GBps"][0][1] > 0 and links["rates_GBps"][1][0] > 0 and links["rates_GBps"][0][0] is None
+    assert c["halo_route"]["autotune"]["mode"] == "links" and c["halo_route"]["link_cost"] == "measured"
+    assert c["halo_route"]["autotune"]["predicted_ms"] > 0
+    dc = d["decomposition"]
+    for key in ("exchange_only_ms", "exchange_groups_ms_sum", "exchange_link_GBps", "exchange_groups",
+                "compute_only_ms", "t_mix_ms", "delta", "tail_ms", "model_prediction_ms", "model_simulated_ms",
+                "achieved_ms", "bound"):
+        assert key in dc, key
+    assert dc["exchange_only_ms"] > 0 and dc["compute_only_ms"] > 0 and dc["t_mix_ms"] > 0
+    assert len(dc["exchange_groups"]) == c["halo_route"]["groups"]
+    assert all(g["ms"] >= 0 and g["busiest_link_MB"] > 0 for g in dc["exchange_groups"])
+    assert c["halo_route"]["achieved_critical_ms"] == dc["exchange_groups_ms_sum"]
+    assert dc["achieved_ms"] == d["ms_per_step"]
     assert set(c["budget"]) >= {"total_s", "headline_s", "left_s", "skipped"}
     assert d["roofline"]["job_peak"] == 16000.0 and abs(d["roofline"]["job_frac"] - d["value"] / 16000.0) < 1e-3
     # 1M-element rows: a 9-row window fits the Infinity Cache, so the scattered rate is there too

@@ -103,6 +103,66 @@ def test_relays_spread_the_halo_at_eight_ranks():
     assert routed.critical_elems() <= 0.55 * direct.critical_elems()
 
 
+def _uniform_rates(world, r=50.0):
+    return {(a, b): r for a in range(world) for b in range(world) if a != b}
+
+
+def test_equal_measured_costs_reproduce_the_uniform_plan():
+    """Costs from equal rates scale every load alike: the same routes as no costs at all."""
+    from federated_amd.halo import link_costs_from_rates
+    tr = ring_transfers(8, 16, 4, 4, 25_000_000)
+    costs = link_costs_from_rates(_uniform_rates(8))
+    assert set(costs.values()) == {16}
+    assert RoutePlan(8, tr, relay=True, link_cost=costs).digest() == RoutePlan(8, tr, relay=True).digest()
+
+
+@pytest.mark.parametrize("slow", [(0, 1), (3, 2), (7, 0)])
+def test_slow_link_sheds_pieces_and_keeps_pairing(slow):
+    """Round-4 review item 2: with one directed link measured at a quarter of the others' rate,
+    the measured-cost plan moves pieces off it (it carries less than on the uniform plan and less
+    than the other neighbour links), the send/recv pairing and coverage invariants still hold, and
+    its predicted exchange time at the measured rates beats the uniform plan's."""
+    from federated_amd.halo import link_costs_from_rates
+    world = 8
+    tr = ring_transfers(world, 16, 4, 4, 25_000_000)
+    rates = _uniform_rates(world)
+    rates[slow] = 12.5
+    costs = link_costs_from_rates(rates)
+    assert costs[slow] == 64 and costs[(slow[1], slow[0])] == 16
+    uniform = RoutePlan(world, tr, relay=True)
+    measured = RoutePlan(world, tr, relay=True, link_cost=costs)
+    _check_plan(measured)
+    assert measured.link_elems[slow] < 0.5 * uniform.link_elems[slow]
+    others = [measured.link_elems[(a, (a + 1) % world)] for a in range(world) if (a, (a + 1) % world) != slow]
+    assert measured.link_elems[slow] < min(others)
+    assert measured.predicted_ms(rates) < 0.8 * uniform.predicted_ms(rates)
+    assert measured.critical_cost() <= RoutePlan(world, tr, relay=False, link_cost=costs).critical_cost()
+    # the same costs give the same plan on every rank
+    assert RoutePlan(world, tr, relay=True, link_cost=dict(costs)).digest() == measured.digest()
+
+
+def test_direct_only_plan_with_a_slow_link_predicts_its_time():
+    """Without relays the slow link's group sets the time: predicted_ms at the measured rates is
+    the busiest group's bytes over the slow rate (the relay option is what removes it)."""
+    world = 4
+    tr = [t for t in ring_transfers(world, 8, 1, 1, 1_000_000)]
+    tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
+    rates = _uniform_rates(world, 40.0)
+    rates[(1, 2)] = 10.0
+    plan = RoutePlan(world, tr, relay=False)
+    assert plan.predicted_ms(rates) == pytest.approx(1_000_000 * 4 / 10e9 * 1e3)
+    assert plan.predicted_ms(_uniform_rates(world, 40.0)) == pytest.approx(1_000_000 * 4 / 40e9 * 1e3)
+
+
+def test_link_costs_reject_nonpositive_rates():
+    from federated_amd.halo import link_costs_from_rates
+    with pytest.raises(ValueError):
+        link_costs_from_rates({(0, 1): 10.0, (1, 0): 0.0})
+    assert link_costs_from_rates({}) == {}
+    with pytest.raises(ValueError):
+        RoutePlan(2, ring_transfers(2, 4, 1, 1, 100), link_cost={(0, 1): 0})
+
+
 def test_route_shares_units_and_order():
     demand = {(0, a, (a + 1) % 6): 1000 for a in range(6)}
     shares, load = route_shares(6, demand, units=16, relay=True)
