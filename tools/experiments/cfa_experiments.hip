@@ -1,7 +1,11 @@
-// cfa_experiments.hip — measurement-only kernels, built into lib/libcfa_exp.so for tools/ (never
-// loaded by the product): cache-policy, traversal-order, read/write decomposition and
-// write-batching variants of the 8-neighbour mix, and allocations with explicit hipExtMalloc
-// flags. Results are recorded under profiles/ (DESIGN.md section 3).
+// cfa_experiments.hip — measurement-only kernels, built into lib/libcfa_exp.so by `make exp` for
+// tools/ (never loaded by the product, not part of the product build): cache-policy,
+// traversal-order and read/write decomposition variants of the 8-neighbour mix, allocations with
+// explicit hipExtMalloc flags or the VMM API, the contention stand-in, completion-signal forms and
+// the read:write ceiling kernels. Results are recorded under profiles/ (DESIGN.md section 3).
+// Variants that were tried and not kept (write batching, one-launch multi-device mix, software-
+// pipelined mix, the fp64-reciprocal division before it moved into the product) were removed in
+// round 5; their code is in commit 27eae93 and their measurements stay under profiles/.
 #include "cfa_internal.h"
 
 extern "C" __attribute__((visibility("default"))) const char* cfa_exp_last_error(void) {
@@ -150,96 +154,6 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_buf(
   return fail(CFA_E_INVALID, "policy pair not instantiated");
 }
 
-// Write-batching experiment: each wave folds B tiles (loads of all 9 streams per tile), keeps
-// the B outputs in registers, then stores them in one burst. SOFT: after each batch's reads, the
-// workgroup waits (bounded spin, never needed for correctness) until every workgroup has
-// finished its reads of that batch, so the chip's write bursts line up in time.
-namespace {
-__device__ unsigned int g_batch_arrivals;
-__global__ void reset_arrivals_kernel() { g_batch_arrivals = 0; }
-
-template <int B, bool SOFT>
-__global__ __launch_bounds__(kBlock) void mix8_batch_kernel(float* out, Fanin f, long long nvec,
-                                                            int spin_limit) {
-  constexpr int N = 8, U = 4;
-  __shared__ f4 ybuf[B][U][kBlock];  // thread-private slots: no LDS synchronisation needed
-  __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
-  constexpr long long kTile = (long long)kBlock * U;
-  const long long full = nvec / kTile;
-  const long long G = gridDim.x;
-  unsigned phase = 0;
-  for (long long t0 = blockIdx.x; t0 < full; t0 += G * B, ++phase) {
-#pragma unroll 1
-    for (int b = 0; b < B; ++b) {
-      const long long t = t0 + b * G;
-      if (t < full) {
-        const long long base = t * kTile + threadIdx.x;
-        f4 v[U][N + 1];
-#pragma unroll
-        for (int k = 0; k <= N; ++k)
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
-#pragma unroll
-        for (int u = 0; u < U; ++u) ybuf[b][u][threadIdx.x] = fold<N, CFA_RULE_SEQUENTIAL>(v[u], f);
-      }
-    }
-    if constexpr (SOFT) {
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(&g_batch_arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned target = (phase + 1) * (unsigned)G;
-        for (int i = 0; i < spin_limit; ++i) {
-          if (__hip_atomic_load(&g_batch_arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const long long t = t0 + b * G;
-      if (t < full) {
-        const long long base = t * kTile + threadIdx.x;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, ybuf[b][u][threadIdx.x]), w,
-                                                 (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
-      }
-    }
-  }
-}
-}  // namespace
-
-extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_batch(
-    float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
-    int batch, int soft, int spin_limit, int blocks_per_cu, void* stream) {
-  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
-  if (spin_limit < 0 || spin_limit > 100000) return fail(CFA_E_INVALID, "spin_limit out of range");
-  Fanin f{};
-  f.src[0] = local;
-  for (int j = 0; j < 8; ++j) {
-    f.src[j + 1] = nbrs[j];
-    f.c[j + 1] = alphas[j];
-  }
-  const long long nvec = (long long)P / 4;
-  cfa_launch_t lc{blocks_per_cu, 4, 0};
-  const unsigned grid = grid_for(nvec / (kBlock * 4), lc);
-  hipStream_t st = (hipStream_t)stream;
-  if (soft) {
-    reset_arrivals_kernel<<<1, 1, 0, st>>>();
-    if (int rc = check_launch("reset_arrivals")) return rc;
-  }
-#define CFA_B(BB)                                                                              \
-  if (batch == BB) {                                                                           \
-    if (soft) mix8_batch_kernel<BB, true><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);  \
-    else mix8_batch_kernel<BB, false><<<grid, kBlock, 0, st>>>(out, f, nvec, spin_limit);      \
-    return check_launch("mix8_batch");                                                         \
-  }
-  CFA_B(1) CFA_B(2) CFA_B(4)
-#undef CFA_B
-  return fail(CFA_E_INVALID, "batch must be 1, 2 or 4");
-}
-
 extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_traverse(
     float* out, const float* local, const float* const* nbrs, const float* alphas, size_t P,
     int mode, int blocks_per_cu, void* stream) {
@@ -343,63 +257,6 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_vmm_free(
   return CFA_OK;
 }
 
-
-// Experiment (not part of the public header): a whole run of ring-window devices mixed in ONE
-// streaming launch. Workgroups walk the (device, tile) space in order, so there is one launch
-// ramp per run instead of one per device; every device's sources are computed from the stack
-// base, the row pitch and the ring wrap-around (no pointer table). Same loads, fold and
-// write-through store as the production mix_vec_kernel<8, SEQ, 4, true>, so the output is
-// identical. For tools/probe/multi_mix.py.
-namespace {
-__global__ __launch_bounds__(kBlock) void mix8_multi_kernel(const float* models, float* outs,
-                                                            long long pitch, int L, int d0,
-                                                            unsigned tiles_per_dev, unsigned total,
-                                                            Fanin f, long long nvec) {
-  constexpr int U = 4;
-  constexpr long long kTile = (long long)kBlock * U;
-  for (unsigned t = blockIdx.x; t < total; t += gridDim.x) {
-    const unsigned rel = t / tiles_per_dev;
-    const int d = d0 + (int)rel;
-    const long long base = (long long)(t - rel * tiles_per_dev) * kTile + threadIdx.x;
-    const float* src[9];
-    src[0] = models + (long long)d * pitch;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int o = j < 4 ? j - 4 : j - 3;  // -4..-1, 1..4: the window order of the reference
-      src[j + 1] = models + (long long)(((d + o) % L + L) % L) * pitch;
-    }
-    f4 v[U][9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(src[k], base + (long long)u * kBlock);
-    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(outs + (long long)d * pitch), 0, (unsigned)(nvec * 16), 0x00020000);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const f4 y = fold<8, CFA_RULE_SEQUENTIAL>(v[u], f);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
-                                             (int)((base + (long long)u * kBlock) * 16), 0, kStoreSc1);
-    }
-  }
-}
-}  // namespace
-
-extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix8_multi(
-    float* outs, const float* models, size_t pitch, int L, int d0, int nd, const float* alphas,
-    size_t P, int blocks_per_cu, void* stream) {
-  if (P % 4096 || P * 4 > 0xffffffffull) return fail(CFA_E_INVALID, "experiment needs P %% 4096 == 0, < 4 GiB");
-  if (L < 9 || d0 < 0 || nd < 1 || d0 + nd > L || pitch < P) return fail(CFA_E_INVALID, "bad run");
-  Fanin f{};
-  for (int j = 0; j < 8; ++j) f.c[j + 1] = alphas[j];
-  const long long nvec = (long long)P / 4;
-  const unsigned tiles = (unsigned)(nvec / (kBlock * 4));
-  const unsigned total = tiles * (unsigned)nd;
-  const unsigned grid = (unsigned)(device_cus() * (blocks_per_cu > 0 ? blocks_per_cu : 2));
-  mix8_multi_kernel<<<grid, kBlock, 0, (hipStream_t)stream>>>(models, outs, (long long)pitch, L, d0,
-                                                              tiles, total, f, nvec);
-  return check_launch("mix8_multi");
-}
 
 // ------------------------------------------------------------------------------------------
 // Contention experiment (tools/probe/contention.py): how much do the mixes of a round slow down
@@ -525,110 +382,6 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_compress(
   CFA_C(4, 1, 0) CFA_C(4, 0, 1) CFA_C(4, 0, 0) CFA_C(2, 1, 0) CFA_C(8, 1, 0)
 #undef CFA_C
   return fail(CFA_E_INVALID, "variant not instantiated");
-}
-
-// ------------------------------------------------------------------------------------------
-// Software-pipelining experiment (tools/probe/pipe_mix.py): the production mix_vec_kernel issues
-// every load of a tile, folds it, stores it, and only then issues the next tile's loads, so with
-// one wave per SIMD the memory pipe idles while a tile folds and stores. Here the loads of the
-// workgroup's NEXT tile are issued before the current tile is folded (two register sets, the loop
-// unrolled by two so no copies; branches only ahead of the loads, so each fold waits with a
-// vmcnt that leaves the next tile's loads in flight). Same loads (nt), fold and sc1 store as the
-// production kernel: the output is identical. RULE 0 sequential, 2 divisor fold.
-// ------------------------------------------------------------------------------------------
-namespace {
-template <int N, int U>
-__device__ __forceinline__ void pipe_load(f4 (&v)[U][N + 1], const Fanin& f, long long base) {
-#pragma unroll
-  for (int k = 0; k <= N; ++k)
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
-  // keep the fold of the previous tile from being scheduled in between these loads (it would
-  // put a wait for the previous tile's data ahead of the remaining loads)
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int N, int RULE, int U, int SAUX>
-__device__ __forceinline__ void pipe_fold_store(const f4 (&v)[U][N + 1], const Fanin& f,
-                                                __amdgpu_buffer_rsrc_t w, long long base) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const f4 y = fold<N, RULE>(v[u], f);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y), w,
-                                           (int)((base + (long long)u * kBlock) * 16), 0, SAUX);
-  }
-}
-template <int N, int RULE, int U, int SAUX = kStoreSc1>
-__global__ __launch_bounds__(kBlock) void mix_pipe_kernel(float* out, Fanin f, long long nvec) {
-  constexpr long long kTile = (long long)kBlock * U;
-  const long long full = nvec / kTile;
-  const long long G = gridDim.x;
-  const __amdgpu_buffer_rsrc_t w =
-      __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
-  f4 a[U][N + 1], b[U][N + 1];
-  // tiles of this workgroup: blockIdx.x + i * G for i < nt. The steady-state loop has no branch
-  // inside (a branch would merge the wait-count state of its paths and make the compiler wait
-  // for the in-flight tile at the loop head); the last one or two tiles are peeled.
-  const long long t0 = blockIdx.x;
-  const long long nt = t0 < full ? (full - 1 - t0) / G + 1 : 0;
-  const long long lane = threadIdx.x;
-  if (nt > 0) {
-    pipe_load<N, U>(a, f, t0 * kTile + lane);
-    long long i = 0;
-    for (; i + 2 < nt; i += 2) {
-      pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
-      pipe_load<N, U>(a, f, (t0 + (i + 2) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U, SAUX>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
-    }
-    if (nt - i == 2) {
-      pipe_load<N, U>(b, f, (t0 + (i + 1) * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
-      pipe_fold_store<N, RULE, U, SAUX>(b, f, w, (t0 + (i + 1) * G) * kTile + lane);
-    } else {
-      pipe_fold_store<N, RULE, U, SAUX>(a, f, w, (t0 + i * G) * kTile + lane);
-    }
-  }
-  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
-    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
-      f4 v[N + 1];
-#pragma unroll
-      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
-      st4<false>(out, i, fold<N, RULE>(v, f));
-    }
-  }
-}
-}  // namespace
-
-// rule 0: w <- w + c_j (x_j - w); rule 2: w <- w + (c_j (x_j - w)) / d_j. n = 8 only (the
-// headline fan-in); P % 4 == 0 and P * 4 < 2 GiB (one buffer-store range).
-extern "C" __attribute__((visibility("default"))) int cfa_experimental_mix_pipe(
-    float* out, const float* local, const float* const* nbrs, const float* coeff, const float* divisors,
-    size_t P, int rule, int u, int blocks_per_cu, void* stream) {
-  if (P % 4 || P * 4 > 0x7ffffff0ull || !out || !local || !nbrs || !coeff)
-    return fail(CFA_E_INVALID, "pipe experiment: P %% 4, P * 4 < 2 GiB, non-null buffers");
-  Fanin f{};
-  f.src[0] = local;
-  f.d[0] = 1.0f;
-  for (int j = 0; j < 8; ++j) {
-    f.src[j + 1] = nbrs[j];
-    f.c[j + 1] = coeff[j];
-    f.d[j + 1] = divisors ? divisors[j] : 1.0f;
-  }
-  set_reciprocals(f, 8);
-  const long long nvec = (long long)P / 4;
-  cfa_launch_t lc{blocks_per_cu, 4, 0};
-  const unsigned grid = grid_for(nvec / (kBlock * u), lc);
-  hipStream_t st = (hipStream_t)stream;
-#define CFA_P(R, U) \
-  if (rule == R && u == U) { mix_pipe_kernel<8, R, U><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix_pipe"); }
-  CFA_P(0, 1) CFA_P(0, 2) CFA_P(0, 4) CFA_P(2, 1) CFA_P(2, 2)
-#undef CFA_P
-  // rule + 10: the same with a nontemporal store
-#define CFA_PN(R, U) \
-  if (rule == R + 10 && u == U) { mix_pipe_kernel<8, R, U, kStoreNt><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("mix_pipe"); }
-  CFA_PN(0, 2) CFA_PN(2, 1) CFA_PN(2, 2)
-#undef CFA_PN
-  return fail(CFA_E_INVALID, "pipe variant not instantiated");
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1318,84 +1071,4 @@ extern "C" __attribute__((visibility("default"))) int cfa_experimental_rw(
 #undef CFA_RW_SHAPES
 #undef CFA_RW
   return fail(CFA_E_INVALID, "rw variant not instantiated");
-}
-
-// ------------------------------------------------------------------------------------------
-// Round 4: the fp32 divisor fold with the division done as ONE fp64 multiply by RN_d(1/d)
-// (tools/probe/lowrow_sweep.py --only div): for fp32 a and d, (float)((double)a * RN_d(1/(double)d))
-// is exactly IEEE a / d -- the exact quotient of two 24-bit values lies at least 2^-50 (relative)
-// from every fp32 rounding midpoint, and the two fp64 roundings stay within 2^-52 of it -- with no
-// range guard (fp64's exponent range covers every fp32 quotient, subnormal or overflowing). Checked
-// on the CPU over 10^9 values and every binade. Against the production Markstein form (three fp32
-// operations plus a range test per float4): two conversions and one fp64 multiply, branch-free.
-// Same skeleton as mix_vec_kernel (full tiles, nt loads, sc1 buffer store).
-// ------------------------------------------------------------------------------------------
-namespace {
-struct DivFanin {
-  const float* src[CFA_MAX_FANIN + 1];
-  float c[CFA_MAX_FANIN + 1];
-  double rd[CFA_MAX_FANIN + 1];
-};
-template <int N>
-__device__ __forceinline__ f4 fold_div64(const f4 (&v)[N + 1], const DivFanin& f) {
-  f4 w = v[0];
-#pragma unroll
-  for (int j = 1; j <= N; ++j) {
-    f4 t = v[j] - w;
-    t = f.c[j] * t;
-    t.x = (float)((double)t.x * f.rd[j]);
-    t.y = (float)((double)t.y * f.rd[j]);
-    t.z = (float)((double)t.z * f.rd[j]);
-    t.w = (float)((double)t.w * f.rd[j]);
-    w = w + t;
-  }
-  return w;
-}
-template <int N, int U, int SP>
-__global__ __launch_bounds__(kBlock) void div64_kernel(float* out, DivFanin f, long long nvec) {
-  constexpr long long kTile = (long long)kBlock * U;
-  const long long full = nvec / kTile;
-  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, (unsigned)(nvec * 16), 0x00020000);
-  f4* o = reinterpret_cast<f4*>(out);
-  for (long long t = blockIdx.x; t < full; t += gridDim.x) {
-    const long long base = t * kTile + threadIdx.x;
-    f4 v[U][N + 1];
-#pragma unroll
-    for (int k = 0; k <= N; ++k)
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u][k] = ld4<true>(f.src[k], base + (long long)u * kBlock);
-#pragma unroll
-    for (int u = 0; u < U; ++u) x_store<f4, SP>(o, w, base + (long long)u * kBlock, fold_div64<N>(v[u], f));
-  }
-  if (blockIdx.x == (unsigned)(full % gridDim.x)) {
-    for (long long i = full * kTile + threadIdx.x; i < nvec; i += kBlock) {
-      f4 v[N + 1];
-#pragma unroll
-      for (int k = 0; k <= N; ++k) v[k] = ld4<false>(f.src[k], i);
-      o[i] = fold_div64<N>(v, f);
-    }
-  }
-}
-}  // namespace
-
-extern "C" __attribute__((visibility("default"))) int cfa_experimental_div64(
-    float* out, const float* local, const float* const* nbrs, const float* alphas, const float* divisors, size_t P,
-    int u, int sp, int bpc, void* stream) {
-  if (P % 4 || P * 4 > 0x7ffffff0ull) return fail(CFA_E_INVALID, "div64 experiment: P %% 4, < 2 GiB");
-  DivFanin f{};
-  f.src[0] = local;
-  for (int j = 1; j <= 8; ++j) {
-    f.src[j] = nbrs[j - 1];
-    f.c[j] = alphas[j - 1];
-    f.rd[j] = 1.0 / (double)divisors[j - 1];
-  }
-  const long long nvec = (long long)P / 4;
-  cfa_launch_t lc{bpc, 4, 0};
-  const unsigned grid = grid_for(std::max(1LL, nvec / (kBlock * u)), lc);
-  hipStream_t st = (hipStream_t)stream;
-#define CFA_D(U, S) \
-  if (u == U && sp == S) { div64_kernel<8, U, S><<<grid, kBlock, 0, st>>>(out, f, nvec); return check_launch("div64"); }
-  CFA_D(1, 3) CFA_D(2, 3) CFA_D(1, 1) CFA_D(2, 1) CFA_D(4, 3) CFA_D(1, 2) CFA_D(2, 2)
-#undef CFA_D
-  return fail(CFA_E_INVALID, "div64 variant not instantiated");
 }

@@ -12,6 +12,7 @@
 #   fetch      rocprofv3 --pmc FETCH_SIZE of the bench command     -> gpurun_out/pmc_TAG/
 #   write      rocprofv3 --pmc WRITE_SIZE of the bench command     -> gpurun_out/pmc_TAG/
 #   rooflines  tools/kernel_rooflines.py (event-timed roofline of every streaming kernel)
+#   rlprof     the same under rocprofv3 --kernel-trace --stats -> gpurun_out/rlprof_TAG/
 #   pmcrows    tools/pmc_rows.py (PMC bytes + VALU busy of the named low-roofline kernels)
 #   py:FILE    python FILE (a tools/ script), e.g. py:tools/dropin_latency.py
 #   ab:NAME    same-box A/B, alternating processes, ROUNDS (default 2) rounds of each side:
@@ -91,6 +92,7 @@ for s in "$@"; do
     fetch) step fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_$TAG" -o fetch --output-format csv -- python3 $BENCH ;;
     write) step write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_$TAG" -o write --output-format csv -- python3 $BENCH ;;
     rooflines) step rooflines 500 python tools/kernel_rooflines.py ;;
+    rlprof) step rlprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rlprof_$TAG" -o rl --output-format csv -- python3 tools/kernel_rooflines.py ;;
     pmcrows) step pmcrows 900 python tools/pmc_rows.py --out "$OUT/pmc_rows_$TAG" ;;
     py:*) f=${s#py:}; step "$(basename "$f" .py)" 600 python "$f" ;;
     ab:*) ab "${s#ab:}" ;;

@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--params", type=int, default=25_000_000)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--passes", type=int, default=3)
-    ap.add_argument("--only", default="fold,mewma,compress,div,ceilings")
+    ap.add_argument("--only", default="fold,mewma,compress,ceilings")
     a = ap.parse_args()
     from federated_amd import _lib
     from federated_amd.engine import get_engine
@@ -182,31 +182,6 @@ def main():
             variants.append((f"bpc={bpc} u={u} sp={sp} ntl={ntl}", fn, (bpc, u)))
         sweep("cfa_compress_epilogue_f32 (mode 2)", 3 * P * 4, variants, R, a.passes, 2)
         del y0, loc, y, yr
-        torch.cuda.empty_cache()
-    if "div" in only:
-        # the fp32 FedAvg divisor fold, n = 8, a divisor that is not a power of two (C = 7)
-        n = 8
-        loc, out, ref = f32(), torch.empty(P, device="cuda"), torch.empty(P, device="cuda")
-        nb = [f32() for _ in range(n)]
-        al, dv = [0.9] * n, [7.0] * n
-        tb = _lib.ptr_table([x.data_ptr() for x in nb])
-        af, df = _lib.float_array(al), _lib.float_array(dv)
-        prod = lambda: eng.mix_seq_div(out, loc, nb, al, dv)
-        prod()
-        torch.cuda.synchronize()
-        ref.copy_(out)
-        variants = [("production (own shape; Markstein division before fe0073c, fp64-reciprocal after)", prod, None)]
-        for bpc, u, sp in [(2, 1, 3), (1, 2, 3), (2, 2, 3), (4, 1, 3), (1, 4, 3), (2, 1, 1), (1, 2, 2), (4, 2, 3)]:
-            fn = (lambda bpc=bpc, u=u, sp=sp: call("cfa_experimental_div64", vp(out.data_ptr()), vp(loc.data_ptr()),
-                                                   tb, af, df, ctypes.c_size_t(P), u, sp, bpc, vp(sh)))
-            out.zero_()
-            fn()
-            torch.cuda.synchronize()
-            if not torch.equal(out, ref):
-                raise SystemExit(f"div64 variant bpc={bpc} u={u} sp={sp} differs from production")
-            variants.append((f"fp64-reciprocal division bpc={bpc} u={u} sp={sp}", fn, (bpc, u)))
-        sweep("cfa_mix_seq_div_f32 (FedAvg divisor fold, n=8, C=7)", (n + 2) * P * 4, variants, R, a.passes, n + 1)
-        del loc, out, ref, nb
         torch.cuda.empty_cache()
     if "ceilings" in only:
         # (label, reads, writes, writes in place over the first reads)
