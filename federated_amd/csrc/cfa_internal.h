@@ -176,32 +176,41 @@ struct Fanin {
   double rd[CFA_MAX_FANIN + 1];         // SEQ_DIV: rd[j] = RN_64(1 / d[j]) (div4_rn)
 };
 
-// Correctly rounded fp32 a / b as one fp64 multiply: p = (double)a * RN_64(1/b) rounded to fp32
-// is IEEE a / b whenever the quotient is a NORMAL fp32 (or zero, infinite, NaN). The exact
-// quotient of two 24-bit significands then lies at least 2^-48 (relative) from every fp32
-// rounding midpoint, while the two fp64 roundings (of 1/b and of the product) stay within 2^-52
-// of it; fp64's exponent range holds every fp32 quotient, so overflow happens in the final
-// conversion as in the IEEE division, and zeros, infinities and NaN propagate as they do there
-// (0 * inf = NaN for 0/0, x * 0 = 0 for x/inf). A SUBNORMAL quotient has fewer significand bits
-// and can sit exactly on a midpoint (a = odd k * o * 2^-149, b = 2o): there the fp64 error of
-// RN(1/b) decides the rounding instead of ties-to-even, so 0 < |p| < 2^-126 takes the IEEE fp32
-// division (never on the bench's buckets; the lanes that take it are exec-masked). Round 4
-// replaced Markstein's three fp32 operations plus a range test per float4 with the one-multiply
-// form (profiles/r04_div64_sweep.jsonl: 0.733 -> 0.776 of peak at 25M, n = 8). Tested bit for
-// bit against numpy over every binade and on exact subnormal ties (tests/test_gpu_kernels.py
-// test_mix_seq_div_*; the rule itself on the CPU, tests/test_div64_rule.py).
-__device__ __forceinline__ float div_rd(float a, double rb, float b) {
-  const double p = (double)a * rb;
-  const double m = __builtin_fabs(p);
-  if (m < 0x1p-126 && m != 0.0) return a / b;
-  return (float)p;
-}
-__device__ __forceinline__ f4 div4_rn(f4 a, double rb, float b) {
+// Correctly rounded fp32 a / b as one fp64 multiply: q = (float)((double)a * RN_64(1/b)) is IEEE
+// a / b whenever the exact quotient is not an exact SUBNORMAL rounding midpoint. Away from a
+// midpoint the exact quotient of two 24-bit significands lies at least 2^-48 (relative) from it,
+// while the two fp64 roundings (of 1/b and of the product) stay within 2^-52: the conversion
+// rounds the right way, normal or subnormal, and fp64's exponent range holds every fp32 quotient
+// (overflow happens in the conversion as in the IEEE division; zeros, infinities and NaN
+// propagate as there). A subnormal quotient has fewer significand bits and CAN sit exactly on a
+// midpoint (a = odd k * o * 2^-149, b = 2o): there the fp64 error of RN(1/b) decides the rounding
+// instead of ties-to-even (round-4 advisor finding). Such a quotient converts to a subnormal fp32
+// (or to 0 only when it is below the 2^-150 tie, which rounds to 0 anyway; the tie below 2^-126
+// rounds up to the normal 2^-126, which ties-to-even also gives), so each step records whether
+// any of its results is subnormal (one v_cmp_class per element, OR-ed on the scalar unit), and a
+// fold that saw one redoes its tile with the IEEE division (fold below: one exec-masked branch per
+// tile, never taken on the bench's buckets). Round 4 replaced Markstein's three fp32 operations
+// plus a range test per float4 with the one-multiply form (profiles/r04_div64_sweep.jsonl: 0.733
+// -> 0.776 of peak at 25M, n = 8). Tested bit for bit against numpy over every binade and on exact
+// subnormal ties (tests/test_gpu_kernels.py test_mix_seq_div_*; the rule itself on the CPU,
+// tests/test_div64_rule.py).
+constexpr int kFcSubnormal = 0x0090;  // __builtin_isfpclass: negative | positive subnormal
+__device__ __forceinline__ f4 div4_rn(f4 a, double rb, bool& subnormal) {
   f4 q;
-  q.x = div_rd(a.x, rb, b);
-  q.y = div_rd(a.y, rb, b);
-  q.z = div_rd(a.z, rb, b);
-  q.w = div_rd(a.w, rb, b);
+  q.x = (float)((double)a.x * rb);
+  q.y = (float)((double)a.y * rb);
+  q.z = (float)((double)a.z * rb);
+  q.w = (float)((double)a.w * rb);
+  subnormal = subnormal | __builtin_isfpclass(q.x, kFcSubnormal) | __builtin_isfpclass(q.y, kFcSubnormal) |
+              __builtin_isfpclass(q.z, kFcSubnormal) | __builtin_isfpclass(q.w, kFcSubnormal);
+  return q;
+}
+__device__ __forceinline__ f4 div4_ieee(f4 a, float b) {
+  f4 q;
+  q.x = a.x / b;
+  q.y = a.y / b;
+  q.z = a.z / b;
+  q.w = a.w / b;
   return q;
 }
 
@@ -236,12 +245,23 @@ __device__ __forceinline__ f4 fold(const f4 (&v)[N + 1], const Fanin& f) {
     return w;
   } else if constexpr (RULE == CFA_RULE_SEQUENTIAL_DIV) {
     f4 w = v[0];
+    bool subnormal = false;
 #pragma unroll
     for (int j = 1; j <= N; ++j) {
       f4 t = v[j] - w;  // numpy: (x - w)
       t = f.c[j] * t;   //        u * (...)
-      t = div4_rn(t, f.rd[j], f.d[j]);  // (...) / C, IEEE-correct fp32 division
+      t = div4_rn(t, f.rd[j], subnormal);  // (...) / C, one fp64 multiply
       w = w + t;
+    }
+    if (__builtin_expect(subnormal, 0)) {  // a subnormal quotient may be an exact tie: IEEE division
+      w = v[0];
+#pragma unroll
+      for (int j = 1; j <= N; ++j) {
+        f4 t = v[j] - w;
+        t = f.c[j] * t;
+        t = div4_ieee(t, f.d[j]);
+        w = w + t;
+      }
     }
     return w;
   } else {
