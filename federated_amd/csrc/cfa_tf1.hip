@@ -73,15 +73,10 @@ __device__ __forceinline__ void tf1_vec(void* out, const Sc1Out& o, const Tf1Fan
   if constexpr (OUT == kOutF32) {
     const f4 y = {(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
     st16_sc1(o, i, y);
-  } else if ((reinterpret_cast<uintptr_t>(out) & 15) == 0) {
-    // fp64 out: one plain 16-B store per lane (sc1 halves measured 17% slower in round 2); only
-    // on a 16-B aligned bucket (a uniform test of the kernel argument)
+  } else {  // fp64 out: one plain 16-B store per lane (sc1 halves measured 17% slower in round 2);
+            // mix_tf1_impl sends an fp64 output whose body is not 16-B aligned to the scalar kernel
     const d2 y = {w[0], w[1]};
     reinterpret_cast<d2*>(out)[i] = y;
-  } else {  // an fp64 view that starts at an odd element: the bucket is only 8-B aligned
-    double* q = reinterpret_cast<double*>(out) + 2 * i;
-    q[0] = w[0];
-    q[1] = w[1];
   }
 }
 
@@ -583,6 +578,14 @@ int mix_tf1_impl(void* out, bool out64, const float* local, const float* const* 
                   "bucket (cfa_mix_tf1_ex_f32)", fn, n, CFA_MAX_FANIN);
     CFA_HIP_CHECK(hipMallocAsync((void**)&scratch, P * sizeof(double), st));
     owned = true;
+  }
+  // The vector kernel stores an fp64 output (the fp64 out, or the scratch of chained passes) as
+  // 16-B vectors, so that output's body must start 16-B aligned; such buckets only promise 8 B
+  // (an fp64 view at an odd element), and then the scalar kernel takes the whole bucket.
+  auto body16 = [&](const void* p) { return ((addr(p) + 8 * head) & 15) == 0; };
+  if (nvec && ((out64 && !body16(out)) || (n > CFA_MAX_FANIN && !body16(scratch)))) {
+    head = P;
+    nvec = 0;
   }
   int rc = CFA_OK;
   for (int done = 0; done < n && rc == CFA_OK;) {
