@@ -1097,27 +1097,7 @@ def main():
         scat = timed_scattered(shard, args.steps)
     t_headline = time.perf_counter() - t_head0
 
-    # N > 1: the headline round taken apart on the headline's own shard (exchange only, compute
-    # only, the model's prediction), so a scaling result explains itself; budget-gated (the
-    # headline never is)
-    decomp = None
-    if world > 1 and headline_exchanges and route is not None and not args.no_decomposition:
-        dsteps = args.decomp_steps or min(args.steps, 10)
-        est = decomposition_estimate(elapsed / args.steps, dsteps, args.warmup)
-        if agree_all(budget.left() - 15.0 >= est):
-            watchdog.enter("decomposition (exchange only, compute only)")
-            try:
-                decomp = decompose_round(shard, world, dsteps, args.warmup, avg_ms,
-                                         (probe["result"] or {}).get("rates"),
-                                         bool(getattr(tstate["transport"], "host_staged", False)))
-                decomp["achieved_ms"] = round(elapsed / args.steps * 1e3, 4)
-            except Exception as exc:
-                decomp = {"error": f"{type(exc).__name__}: {exc}"}
-                print(f"[bench rank {rank}] decomposition failed: {decomp['error']}", file=sys.stderr, flush=True)
-            if not agree_all("error" not in decomp):
-                decomp = {"error": decomp.get("error", "failed on another rank")}
-        else:
-            decomp = {"skipped": "budget", "estimate_s": round(est, 1), "budget_left_s": round(budget.left(), 1)}
+    decomp = None  # filled after the line's headline part is built (below)
 
     result = None
     if rank == 0:
@@ -1205,8 +1185,6 @@ def main():
                     shard_P(info, P), K, kernel, args.window_batch or 1),
             },
         }
-        if decomp is not None:
-            result["decomposition"] = decomp
         if scat is not None:
             xel, xdur = scat
             result["value_scattered"] = round(bytes_total / xel / 1e9, 2)
@@ -1234,6 +1212,70 @@ def main():
     reserve = 15.0 + (2 * pmc_est if live else 0.0)
     legs = {}
     leg_failed = False
+
+    import threading
+    report_lock = threading.Lock()
+
+    def report_partial(mark):
+        """Rank 0: print the line once, with what is measured so far and ``mark(out)`` recording
+        the part that did not finish (the headline is complete). Returns the exit status: 5, or 3
+        after a headline fallback. The other ranks give rank 0 time to print first
+        (torch.distributed.run ends every rank once one has exited)."""
+        code = EXIT_TRANSPORT if headline_fallback else EXIT_LEG
+        with report_lock:
+            if rank == 0 and not report_partial.done:
+                out = None
+                for _ in range(50):  # the main thread may be adding a leg right now
+                    try:
+                        out = json.loads(json.dumps(result))
+                        break
+                    except RuntimeError:
+                        time.sleep(0.01)
+                if out is None:
+                    out = {k: v for k, v in result.items() if k != "partitions"}
+                mark(out)
+                out["exit_status"] = code
+                print(json.dumps(out), flush=True)
+                record_status(code)
+                report_partial.done = True
+        if rank != 0:
+            wait_for_status(15.0)
+        return code
+    report_partial.done = False
+
+    # N > 1: the headline round taken apart on the headline's own shard (exchange only, compute
+    # only, the model's prediction), so a scaling result explains itself. Budget-gated (the
+    # headline never is) and run as a leg with its own watchdog budget: if it hangs in a
+    # collective, rank 0 prints the line with the headline and the decomposition's error.
+    if world > 1 and headline_exchanges and route is not None and not args.no_decomposition:
+        dsteps = args.decomp_steps or min(args.steps, 10)
+        est = decomposition_estimate(elapsed / args.steps, dsteps, args.warmup)
+        if agree_all(budget.left() - reserve >= est):
+            seconds = budget.left() - reserve
+            if args.leg_seconds > 0:
+                seconds = min(seconds, args.leg_seconds)
+
+            def decomp_expired(phase, seconds=seconds):
+                why = f"did not finish within {seconds:.0f} s (phase '{phase}')"
+                return report_partial(lambda out: out.__setitem__("decomposition", {"error": why}))
+            watchdog.leg("decomposition (exchange only, compute only)", seconds, decomp_expired)
+            try:
+                decomp = decompose_round(shard, world, dsteps, args.warmup, avg_ms,
+                                         (probe["result"] or {}).get("rates"),
+                                         bool(getattr(tstate["transport"], "host_staged", False)))
+                decomp["achieved_ms"] = round(elapsed / args.steps * 1e3, 4)
+            except Exception as exc:
+                decomp = {"error": f"{type(exc).__name__}: {exc}"}
+                print(f"[bench rank {rank}] decomposition failed: {decomp['error']}", file=sys.stderr, flush=True)
+            if not agree_all("error" not in decomp):
+                decomp = {"error": decomp.get("error", "failed on another rank")}
+            watchdog.end_leg()
+        else:
+            decomp = {"skipped": "budget", "estimate_s": round(est, 1), "budget_left_s": round(budget.left(), 1)}
+        if rank == 0:
+            result["decomposition"] = decomp
+            result["config"]["halo_route"]["achieved_critical_ms"] = decomp.get("exchange_groups_ms_sum")
+
     if world > 1 and not args.no_extra_legs and not weak:
         del shard
         drop_cached()
@@ -1249,36 +1291,10 @@ def main():
             "weak": f"{args.devices} devices per GPU (population grown with N), devices partition",
         }
 
-        import threading
-        report_lock = threading.Lock()
-
         def report_early(name, why):
-            """Rank 0: print the line once, with the legs measured so far and ``name`` marked with
-            ``why`` (the headline is complete). Returns the exit status: 5, or 3 after a headline
-            fallback. The other ranks give rank 0 time to print first (torch.distributed.run ends
-            every rank once one has exited)."""
-            code = EXIT_TRANSPORT if headline_fallback else EXIT_LEG
-            with report_lock:
-                if rank == 0 and not report_early.done:
-                    out = None
-                    for _ in range(50):  # the main thread may be adding a leg right now
-                        try:
-                            out = json.loads(json.dumps(result))
-                            break
-                        except RuntimeError:
-                            time.sleep(0.01)
-                    if out is None:
-                        out = {k: v for k, v in result.items() if k != "partitions"}
-                        out["partitions"] = {}
-                    out["partitions"][name] = {"error": why, "note": notes[name]}
-                    out["exit_status"] = code
-                    print(json.dumps(out), flush=True)
-                    record_status(code)
-                    report_early.done = True
-            if rank != 0:
-                wait_for_status(15.0)
-            return code
-        report_early.done = False
+            """The line with the legs measured so far and leg ``name`` marked with ``why``."""
+            return report_partial(lambda out: out.setdefault("partitions", {}).__setitem__(
+                name, {"error": why, "note": notes[name]}))
 
         def leg_expired(name, seconds):
             # runs on the watchdog thread of a rank whose leg budget ran out (every rank's budget
