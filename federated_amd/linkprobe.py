@@ -11,7 +11,9 @@ DESIGN.md §5): this module measures them with the same transport and message pa
   directions once over the rounds, while no GPU drives two links at a time.
 * ``probe_links``: per round, each pair exchanges one ``elems``-float message each way, ``reps``
   times after a warm-up, timed with HIP events on the exchange stream (host clock on a
-  host-staged transport); the pair's time is the slower end's. Then an all-peers pass: every rank
+  host-staged transport); the pair's time is the slower end's. The same bytes are then sent as
+  ``pieces`` messages in one group (the routed halo sends pieces of a row, not whole rows): the
+  difference over the extra messages is the per-message cost. Then an all-peers pass: every rank
   sends to and receives from all peers at once (equal chunks), the per-GPU egress rate with every
   link busy together, which says whether the links of one GPU are independent (what the relayed
   routes assume).
@@ -94,11 +96,12 @@ def _timed(op, stream, reps: int, warmup: int, device_timing: bool) -> float:
 
 
 def probe_links(transport, rank: int, world: int, device=None, elems: int = 16 << 20, reps: int = 3,
-                warmup: int = 1, all_peers: bool = True, group=None) -> dict:
+                warmup: int = 1, all_peers: bool = True, group=None, pieces: int = 32) -> dict:
     """Measure every directed link (see the module docstring). Collective over the default
     torch.distributed group (``group``: another control group): every rank calls it with the same
     arguments. Returns {"rates": {(a, b): GB/s}, "pair_ms": [[ms]], "elems": elems,
-    "all_peers": {"egress_GBps": [per rank], "chunk_elems": c} or None} identical on every rank."""
+    "pieces": {"count": pieces, "pair_ms": [[ms]]} or None,
+    "all_peers": {"egress_GBps": [per rank], "chunk_elems": c} or None}, identical on every rank."""
     import torch
     import torch.distributed as dist
 
@@ -110,19 +113,28 @@ def probe_links(transport, rank: int, world: int, device=None, elems: int = 16 <
     recv = torch.empty(elems, dtype=torch.float32, device=dev)
     stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
     device_timing = dev.type == "cuda" and not getattr(transport, "host_staged", False)
-    times = torch.zeros((world, world), dtype=torch.float64)
+    times = torch.zeros((2, world, world), dtype=torch.float64)
+    piece = max(ALIGN, elems // max(1, pieces) // ALIGN * ALIGN) if pieces > 1 else 0
     for pairs in matching_rounds(world):
         dist.barrier(group=group)  # one round at a time: no GPU drives two links
         partner = next((b if a == rank else a for a, b in pairs if rank in (a, b)), None)
         if partner is None:
             continue
         op = _prepare(transport, [(send, partner)], [(recv, partner)])
-        times[rank, partner] = _timed(op, stream, reps, warmup, device_timing)
+        times[0, rank, partner] = _timed(op, stream, reps, warmup, device_timing)
         if float(recv[0].item()) != float(partner):
             raise RuntimeError(f"link probe: rank {rank} received {float(recv[0].item())} from {partner}")
+        if piece:
+            k = elems // piece
+            op = _prepare(transport, [(send[i * piece:(i + 1) * piece], partner) for i in range(k)],
+                          [(recv[i * piece:(i + 1) * piece], partner) for i in range(k)])
+            times[1, rank, partner] = _timed(op, stream, reps, warmup, device_timing) * elems / (k * piece)
     dist.all_reduce(times, op=dist.ReduceOp.SUM, group=group)  # each entry written by one rank
-    res = {"elems": elems, "rates": rates_from_times(times.tolist(), elems),
-           "pair_ms": [[round(float(t) * 1e3, 4) for t in row] for row in times.tolist()], "all_peers": None}
+    t1, tp = times[0].tolist(), times[1].tolist()
+    res = {"elems": elems, "rates": rates_from_times(t1, elems),
+           "pair_ms": [[round(float(t) * 1e3, 4) for t in row] for row in t1], "all_peers": None,
+           "pieces": {"count": elems // piece, "piece_elems": piece,
+                      "pair_ms": [[round(float(t) * 1e3, 4) for t in row] for row in tp]} if piece else None}
     if all_peers and world > 2:
         chunk = max(ALIGN, elems // (world - 1) // ALIGN * ALIGN)
         peers = [p for p in range(world) if p != rank]
@@ -155,6 +167,22 @@ def summarize(probe: dict, world: int) -> dict:
            "min_GBps": round(vals[0], 2) if vals else None,
            "median_GBps": round(statistics.median(vals), 2) if vals else None,
            "max_GBps": round(vals[-1], 2) if vals else None}
+    pc = probe.get("pieces")
+    if pc:
+        # per-message cost: (time as `count` messages - time as one) / (count - 1), per pair
+        extra = []
+        for a in range(world):
+            for b in range(a + 1, world):
+                one = max(probe["pair_ms"][a][b], probe["pair_ms"][b][a])
+                many = max(pc["pair_ms"][a][b], pc["pair_ms"][b][a])
+                if one > 0 and many > 0 and pc["count"] > 1:
+                    extra.append((many - one) / (pc["count"] - 1) * 1e3)
+        out["pieces"] = {"count": pc["count"], "piece_MB": round(pc["piece_elems"] * 4 / 1e6, 2),
+                         "per_message_us_median": round(statistics.median(extra), 2) if extra else None,
+                         "pieces_rate_median_GBps": round(statistics.median(
+                             [probe["elems"] * 4 / (max(pc["pair_ms"][a][b], pc["pair_ms"][b][a]) * 1e-3) / 1e9
+                              for a in range(world) for b in range(a + 1, world)
+                              if max(pc["pair_ms"][a][b], pc["pair_ms"][b][a]) > 0]), 2) if extra else None}
     ap = probe.get("all_peers")
     if ap:
         eg = ap["egress_GBps"]

@@ -78,6 +78,10 @@ def test_probe_links_over_gloo(world):
     assert all(v > 0 for v in first["rates"].values())
     for res in results.values():  # identical on every rank (the route plan must be)
         assert res["rates"] == first["rates"] and res["pair_ms"] == first["pair_ms"]
+    pc = first["pieces"]
+    assert pc["count"] == 32 and all(pc["pair_ms"][a][b] > 0 for a in range(world) for b in range(world) if a != b)
+    s2 = summarize(first, world)
+    assert s2["pieces"]["count"] == 32 and s2["pieces"]["per_message_us_median"] is not None
     if world > 2:
         assert len(first["all_peers"]["egress_GBps"]) == world and all(first["all_peers"]["egress_GBps"])
         s = summarize(first, world)
