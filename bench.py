@@ -953,23 +953,22 @@ def main():
     # Per-link rates of the node, measured over the headline's transport before any route is
     # planned (federated_amd/linkprobe.py): with --route-tune links (default) they become the
     # route plan's link costs, and every line at N > 1 reports them (config.links)
-    probe = {"result": None, "costs": None, "summary": None, "error": None}
+    probe = {"result": None, "plan_rates": None, "summary": None, "error": None}
     if headline_exchanges and args.link_probe_mb > 0 and tstate["transport"] is not None:
         watchdog.enter("link probe")
-        from federated_amd.halo import link_costs_from_rates
         from federated_amd.linkprobe import probe_links, summarize
         t_probe = time.perf_counter()
         try:
             res = probe_links(tstate["transport"], rank, world, device, elems=int(args.link_probe_mb * 1e6 / 4))
             probe.update(result=res, summary=summarize(res, world))
             if route_tune == "links":
-                probe["costs"] = link_costs_from_rates(res["rates"])
+                probe["plan_rates"] = res["rates"]  # the route plan's input (population.make_ring_shard)
         except Exception as exc:
             tail = rccl_log_tail(rccl_log)
             probe["error"] = f"{type(exc).__name__}: {exc}" + (f" [RCCL log: {tail}]" if tail else "")
             print(f"[bench rank {rank}] link probe failed: {probe['error']}", file=sys.stderr, flush=True)
         if not agree_all(probe["error"] is None):
-            probe.update(result=None, costs=None, summary=None, error=probe["error"] or "failed on another rank")
+            probe.update(result=None, plan_rates=None, summary=None, error=probe["error"] or "failed on another rank")
         if probe["summary"] is not None:
             probe["summary"]["wall_s"] = round(time.perf_counter() - t_probe, 2)
 
@@ -981,7 +980,7 @@ def main():
                                       relay=(not args.no_relay) if relay is None else relay,
                                       staged=not args.no_stages, window_batch=args.window_batch,
                                       placement_candidates=args.placement_candidates,
-                                      placement_release=args.placement_release, link_cost=probe["costs"])
+                                      placement_release=args.placement_release, link_rates=probe["plan_rates"])
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -997,19 +996,21 @@ def main():
         if args.placement_release:
             torch.cuda.empty_cache()
 
-    def route_choice(xshard):
-        """How the shard's route was chosen, for halo_route.autotune: with measured link costs the
-        plan itself keeps relays only where they shorten the predicted critical path; its predicted
-        exchange time at the probe's rates beside the direct-only plan's."""
+    def route_choice(xshard, xinfo):
+        """How the shard's route was chosen, for halo_route.autotune: with measured rates
+        (--route-tune links) halo.choose_route priced the uniform, the rate-weighted and the
+        direct plan at the probe's rates and kept the fastest; the chosen plan's predicted exchange
+        time beside the direct-only plan's."""
         plan = xshard._route_plan
+        rc = xinfo.get("route_choice") or {}
         out = {"mode": route_tune, "chosen": "relayed" if plan.relay else "direct",
-               "link_cost": "measured" if plan.link_cost else "uniform"}
+               "plan": rc.get("chosen", "uniform"), "candidates_predicted_ms": rc.get("candidates"),
+               "slow_links": rc.get("slow_links")}
         rates = (probe["result"] or {}).get("rates")
         if rates:
             from federated_amd.halo import RoutePlan
-            direct = RoutePlan(world, plan.transfers, relay=False, link_cost=plan.link_cost)
             out["predicted_ms"] = round(plan.predicted_ms(rates), 4)
-            out["direct_predicted_ms"] = round(direct.predicted_ms(rates), 4)
+            out["direct_predicted_ms"] = round(RoutePlan(world, plan.transfers, relay=False).predicted_ms(rates), 4)
         return out
 
     def build_tuned(partition, devices=None):
@@ -1022,7 +1023,7 @@ def main():
         if not (world > 1 and xinfo.get("route")):
             return xshard, xinfo, None
         if route_tune != "wallclock" or not xinfo["route"].get("relay"):
-            return xshard, xinfo, route_choice(xshard)
+            return xshard, xinfo, route_choice(xshard, xinfo)
         tune_steps = 3
         watchdog.enter(f"route autotune ({partition})")
         t_rel, _, _ = run_leg(args, xshard, world, tune_steps, args.warmup, timed_kernel=False)

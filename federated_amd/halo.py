@@ -346,21 +346,48 @@ class RoutedExchange:
                     stage_done(s)
 
 
-def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int = 16) -> Dict[Tuple[int, int], int]:
-    """Integer per-element cost of each directed link from measured rates: the fastest link costs
-    ``scale``, a link at half its rate 2 * scale (rounded; at least 1). Integer so that every rank
-    plans the same routes from the same (all-reduced) rates."""
+def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int = 16,
+                          tolerance: float = 0.15) -> Dict[Tuple[int, int], int]:
+    """Integer per-element cost of each directed link from measured rates. Links within
+    ``tolerance`` of the median rate (or faster) cost ``scale``: the probe's run-to-run noise must
+    not reshape a plan that is optimal for equal links. A slower link costs scale * median / rate
+    (rounded): a link at half the median rate costs 2 * scale. Integer so that every rank plans the
+    same routes from the same (all-reduced) rates."""
     if not rates_gbps:
         return {}
-    fastest = max(rates_gbps.values())
-    if not fastest > 0:
-        raise ValueError("link rates must be positive")
-    out = {}
-    for l, r in sorted(rates_gbps.items()):
+    vals = sorted(rates_gbps.values())
+    for l, r in rates_gbps.items():
         if not r > 0:
             raise ValueError(f"link {l} has no positive rate ({r})")
-        out[l] = max(1, int(round(scale * fastest / r)))
+    n = len(vals)
+    median = vals[n // 2] if n % 2 else 0.5 * (vals[n // 2 - 1] + vals[n // 2])
+    out = {}
+    for l, r in sorted(rates_gbps.items()):
+        out[l] = scale if r >= (1.0 - tolerance) * median else max(1, int(round(scale * median / r)))
     return out
+
+
+def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
+                 rates_gbps: Optional[Dict[Tuple[int, int], float]] = None,
+                 tolerance: float = 0.15) -> Tuple["RoutePlan", dict]:
+    """The route plan for measured link rates: the uniform plan, the plan weighed by
+    ``link_costs_from_rates`` (when some link is slower than the tolerance) and the direct-only
+    plan, each priced with ``RoutePlan.predicted_ms`` at the measured rates; the fastest is kept
+    (ties to the earlier candidate, in that order). Deterministic: every rank holding the same rates
+    keeps the same plan. Without rates, the uniform plan. Returns (plan, report)."""
+    uniform = RoutePlan(world, transfers, relay=relay)
+    if not rates_gbps:
+        return uniform, {"chosen": "uniform", "candidates": {}}
+    cands = [("uniform", uniform)]
+    costs = link_costs_from_rates(rates_gbps, tolerance=tolerance)
+    if costs and len(set(costs.values())) > 1:
+        cands.append(("measured", RoutePlan(world, transfers, relay=relay, link_cost=costs)))
+    if uniform.relay:
+        cands.append(("direct", RoutePlan(world, transfers, relay=False)))
+    scored = [(p.predicted_ms(rates_gbps), i, name, p) for i, (name, p) in enumerate(cands)]
+    best = min(scored, key=lambda x: (round(x[0], 9), x[1]))
+    return best[3], {"chosen": best[2], "candidates": {name: round(t, 4) for t, _, name, _ in scored},
+                     "slow_links": sorted(f"{a}->{b}" for (a, b), c in costs.items() if c != 16)}
 
 
 def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world: int = 1,

@@ -415,7 +415,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
                     window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
-                    placement_release: bool = False, link_cost=None):
+                    placement_release: bool = False, link_rates=None):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -425,20 +425,22 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     row so boundary devices mix as their rows land (both only matter when Gd > 1).
     ``placement_candidates`` > 1 allocates the shard's stacks placement-calibrated
     (``placement.calibrated_stacks``: the fastest of that many allocations each, timed with the
-    shard's own mix; ``info["placement"]`` holds the probe). ``link_cost``: measured per-link costs
-    for the route plan (``halo.link_costs_from_rates``; None = every link alike)."""
-    from .halo import RoutePlan, ring_transfers
+    shard's own mix; ``info["placement"]`` holds the probe). ``link_rates``: measured per-link rates
+    (GB/s, ``linkprobe.probe_links``): the route is then ``halo.choose_route``'s pick among the
+    uniform, the rate-weighted and the direct plan (``info["route_choice"]``); None = every link
+    alike."""
+    from .halo import choose_route, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
     bounds = slice_bounds(P, gp)
     L = devices // gd
     plan = RingShardPlan(d, gd, L, hl, hr)
-    route = None
+    route, route_choice = None, None
     if gd > 1:
         tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
-        route = RoutePlan(world, tr, relay=relay, link_cost=link_cost)
+        route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates)
     Pr = bounds[p + 1] - bounds[p]
     stacks, placement = None, None
     if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":
@@ -454,4 +456,5 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     if route is not None:
         info["route"] = route.summary()
         info["route_digest"] = route.digest()
+        info["route_choice"] = route_choice
     return shard, info

@@ -75,8 +75,9 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     # round 5: the link probe's measured rates feed the route plan, and the round is decomposed
     links = c["links"]
     assert links["rates_GBps"][0][1] > 0 and links["rates_GBps"][1][0] > 0 and links["rates_GBps"][0][0] is None
-    assert c["halo_route"]["autotune"]["mode"] == "links" and c["halo_route"]["link_cost"] == "measured"
-    assert c["halo_route"]["autotune"]["predicted_ms"] > 0
+    at = c["halo_route"]["autotune"]
+    assert at["mode"] == "links" and at["plan"] in ("uniform", "measured", "direct") and at["predicted_ms"] > 0
+    assert at["candidates_predicted_ms"]["uniform"] > 0 and c["halo_route"]["link_cost"] in ("uniform", "measured")
     dc = d["decomposition"]
     for key in ("exchange_only_ms", "exchange_groups_ms_sum", "exchange_link_GBps", "exchange_groups",
                 "compute_only_ms", "t_mix_ms", "delta", "tail_ms", "model_prediction_ms", "model_simulated_ms",

@@ -154,6 +154,29 @@ def test_direct_only_plan_with_a_slow_link_predicts_its_time():
     assert plan.predicted_ms(_uniform_rates(world, 40.0)) == pytest.approx(1_000_000 * 4 / 40e9 * 1e3)
 
 
+def test_choose_route_keeps_the_fastest_predicted_plan():
+    """halo.choose_route prices the uniform, rate-weighted and direct plans at the measured rates:
+    equal or merely noisy rates (within the 15% tolerance) keep the uniform plan; one slow link
+    picks the rate-weighted plan; every candidate's time is reported."""
+    from federated_amd.halo import choose_route
+    tr = ring_transfers(8, 16, 4, 4, 25_000_000)
+    uniform = RoutePlan(8, tr, relay=True)
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=_uniform_rates(8))
+    assert rep["chosen"] == "uniform" and plan.digest() == uniform.digest()
+    assert set(rep["candidates"]) == {"uniform", "direct"} and rep["slow_links"] == []
+    noisy = {l: 50.0 * (0.9 + 0.02 * ((l[0] * 8 + l[1]) % 10)) for l in _uniform_rates(8)}
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=noisy)
+    assert rep["chosen"] == "uniform" and plan.digest() == uniform.digest()
+    slow = _uniform_rates(8)
+    slow[(2, 3)] = 10.0
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=slow)
+    assert rep["chosen"] == "measured" and rep["slow_links"] == ["2->3"]
+    assert rep["candidates"]["measured"] < rep["candidates"]["uniform"] < rep["candidates"]["direct"]
+    _check_plan(plan)
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=None)
+    assert rep["chosen"] == "uniform" and rep["candidates"] == {}
+
+
 def test_link_costs_reject_nonpositive_rates():
     from federated_amd.halo import link_costs_from_rates
     with pytest.raises(ValueError):
