@@ -1413,6 +1413,14 @@ def main():
                 result["e2e"] = measure_e2e(eng, P, K)
             else:
                 skipped.append("e2e")
+    if world > 1:
+        # every rank's RCCL warnings (NCCL_DEBUG=WARN, setup_rccl_diagnostics) into the line, so a
+        # scaling run on a node this build never ran on says what RCCL complained about
+        watchdog.enter("gather RCCL logs")
+        tails = [None] * world
+        dist.all_gather_object(tails, rccl_log_tail(rccl_log, 600))
+        if rank == 0:
+            result["config"]["rccl_log"] = {str(r): t for r, t in enumerate(tails) if t} or None
     code = EXIT_TRANSPORT if headline_fallback else (EXIT_LEG if leg_failed else 0)
     if rank == 0:
         result["config"]["budget"].update({"skipped": skipped, "left_s": round(budget.left(), 1)})
@@ -1428,6 +1436,11 @@ def main():
         tstate["transport"].close()
     if world > 1:
         dist.destroy_process_group()
+    if rccl_log and os.path.basename(rccl_log).startswith("cfa_rccl_r"):
+        try:
+            os.unlink(rccl_log)  # ours (setup_rccl_diagnostics), its tail is in the line
+        except OSError:
+            pass
     watchdog.done()
     if code:
         sys.exit(code)
