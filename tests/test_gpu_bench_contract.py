@@ -41,7 +41,7 @@ def test_bench_line_contract():
 N_GT_1_FIELDS = [("value", float), ("ms_per_step", float), ("n_gpus", int), ("exit_status", int),
                  ("config", dict), ("roofline", dict), ("partitions", dict)]
 CONFIG_FIELDS = ["partition", "transport", "comparable", "rccl_version", "halo_route", "cache_reuse", "rows_note",
-                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback"]
+                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback", "links", "rccl_log"]
 
 
 def _self_launched(extra, timeout=240):
