@@ -764,7 +764,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     import torch.distributed as dist
     from federated_amd.population import predict_round_ms
 
-    plan = shard._route_plan
+    plan = shard.route_plan
     routed = shard.routed()
     G = len(plan.groups)
     compute = torch.cuda.current_stream()
@@ -1001,7 +1001,7 @@ def main():
         (--route-tune links) halo.choose_route priced the uniform, the rate-weighted and the
         direct plan at the probe's rates and kept the fastest; the chosen plan's predicted exchange
         time beside the direct-only plan's."""
-        plan = xshard._route_plan
+        plan = xshard.route_plan
         rc = xinfo.get("route_choice") or {}
         out = {"mode": route_tune, "chosen": "relayed" if plan.relay else "direct",
                "plan": rc.get("chosen", "uniform"), "candidates_predicted_ms": rc.get("candidates"),

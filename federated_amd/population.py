@@ -320,6 +320,11 @@ class RingPopulationShard:
             if timer:
                 timer(i, False)
 
+    @property
+    def route_plan(self):
+        """The halo.RoutePlan this shard exchanges with (None at world 1)."""
+        return self._route_plan
+
     def compute_round(self, stream=None, timer=None) -> None:
         """Every device's mix and nothing else (the halo rows hold what the last exchange
         delivered): the compute-only round of the bench's N > 1 decomposition. ``timer`` as in
