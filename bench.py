@@ -745,7 +745,7 @@ def decomposition_estimate(step_s: float, steps: int, warmup: int) -> float:
 
 
 def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: float, rates=None,
-                    host_staged: bool = False) -> dict:
+                    host_staged: bool = False, message_us: float = 0.0) -> dict:
     """The N > 1 headline round taken apart on the headline's own shard (round-4 review):
 
     (a) exchange only: the routed halo with no mixes, ``steps`` rounds after ``warmup``, each group
@@ -835,7 +835,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     x_el, c_el, t_mix, delta, sim, simple, compute_bound = vec[:7].tolist()
     group_ms = vec[7:].tolist()
     x_round = sum(group_ms)
-    pred = plan.predicted_group_ms(rates) if rates else [None] * G
+    pred = plan.predicted_group_ms(rates, message_us=message_us) if rates else [None] * G
     groups = []
     for g in range(G):
         busiest = max(plan.group_link_elems(g).values(), default=0) * 4
@@ -953,7 +953,7 @@ def main():
     # Per-link rates of the node, measured over the headline's transport before any route is
     # planned (federated_amd/linkprobe.py): with --route-tune links (default) they become the
     # route plan's link costs, and every line at N > 1 reports them (config.links)
-    probe = {"result": None, "plan_rates": None, "summary": None, "error": None}
+    probe = {"result": None, "plan_rates": None, "message_us": 0.0, "summary": None, "error": None}
     if headline_exchanges and args.link_probe_mb > 0 and tstate["transport"] is not None:
         watchdog.enter("link probe")
         from federated_amd.linkprobe import probe_links, summarize
@@ -963,6 +963,8 @@ def main():
             probe.update(result=res, summary=summarize(res, world))
             if route_tune == "links":
                 probe["plan_rates"] = res["rates"]  # the route plan's input (population.make_ring_shard)
+                probe["message_us"] = max(0.0, (probe["summary"].get("pieces") or {}).get("per_message_us_median")
+                                          or 0.0)
         except Exception as exc:
             tail = rccl_log_tail(rccl_log)
             probe["error"] = f"{type(exc).__name__}: {exc}" + (f" [RCCL log: {tail}]" if tail else "")
@@ -980,7 +982,8 @@ def main():
                                       relay=(not args.no_relay) if relay is None else relay,
                                       staged=not args.no_stages, window_batch=args.window_batch,
                                       placement_candidates=args.placement_candidates,
-                                      placement_release=args.placement_release, link_rates=probe["plan_rates"])
+                                      placement_release=args.placement_release, link_rates=probe["plan_rates"],
+                                      message_us=probe["message_us"])
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -1005,12 +1008,14 @@ def main():
         rc = xinfo.get("route_choice") or {}
         out = {"mode": route_tune, "chosen": "relayed" if plan.relay else "direct",
                "plan": rc.get("chosen", "uniform"), "candidates_predicted_ms": rc.get("candidates"),
-               "slow_links": rc.get("slow_links")}
+               "slow_links": rc.get("slow_links"), "message_us": rc.get("message_us")}
         rates = (probe["result"] or {}).get("rates")
         if rates:
             from federated_amd.halo import RoutePlan
-            out["predicted_ms"] = round(plan.predicted_ms(rates), 4)
-            out["direct_predicted_ms"] = round(RoutePlan(world, plan.transfers, relay=False).predicted_ms(rates), 4)
+            msg = probe["message_us"]
+            out["predicted_ms"] = round(plan.predicted_ms(rates, message_us=msg), 4)
+            out["direct_predicted_ms"] = round(RoutePlan(world, plan.transfers, relay=False).predicted_ms(
+                rates, message_us=msg), 4)
         return out
 
     def build_tuned(partition, devices=None):
@@ -1263,7 +1268,8 @@ def main():
             try:
                 decomp = decompose_round(shard, world, dsteps, args.warmup, avg_ms,
                                          (probe["result"] or {}).get("rates"),
-                                         bool(getattr(tstate["transport"], "host_staged", False)))
+                                         bool(getattr(tstate["transport"], "host_staged", False)),
+                                         probe["message_us"])
                 decomp["achieved_ms"] = round(elapsed / args.steps * 1e3, 4)
             except Exception as exc:
                 decomp = {"error": f"{type(exc).__name__}: {exc}"}

@@ -256,10 +256,22 @@ class RoutePlan:
                          default=0)
         return total
 
-    def predicted_group_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4) -> List[float]:
+    def max_rank_messages(self, group: int) -> int:
+        """The most messages one rank issues in one direction (sends or receives) in ``group``."""
+        sends: Dict[int, int] = defaultdict(int)
+        recvs: Dict[int, int] = defaultdict(int)
+        for m in self.groups[group]:
+            sends[m.src] += 1
+            recvs[m.dst] += 1
+        return max(list(sends.values()) + list(recvs.values()), default=0)
+
+    def predicted_group_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4,
+                           message_us: float = 0.0) -> List[float]:
         """Per group, the time its slowest link needs at the given per-direction rates (GB/s; a link
-        missing from ``rates_gbps`` takes the slowest rate given): the group's length when every
-        link runs at its measured rate and the groups run back to back."""
+        missing from ``rates_gbps`` takes the slowest rate given), plus ``message_us`` per message
+        of the rank that issues the most in the group (the per-message cost the link probe
+        measures): the group's length when every link runs at its measured rate and the groups run
+        back to back."""
         slow = min(rates_gbps.values()) if rates_gbps else None
         out = []
         for g in range(len(self.groups)):
@@ -268,11 +280,14 @@ class RoutePlan:
                 r = rates_gbps.get(l, slow)
                 if r:
                     t = max(t, n * elem_bytes / (r * 1e9) * 1e3)
+            if message_us > 0:
+                t += message_us * 1e-3 * self.max_rank_messages(g)
             out.append(t)
         return out
 
-    def predicted_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4) -> float:
-        return sum(self.predicted_group_ms(rates_gbps, elem_bytes))
+    def predicted_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4,
+                     message_us: float = 0.0) -> float:
+        return sum(self.predicted_group_ms(rates_gbps, elem_bytes, message_us))
 
     def digest(self) -> str:
         h = hashlib.sha1()
@@ -369,24 +384,35 @@ def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int =
 
 def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
                  rates_gbps: Optional[Dict[Tuple[int, int], float]] = None,
-                 tolerance: float = 0.15) -> Tuple["RoutePlan", dict]:
+                 tolerance: float = 0.15, message_us: float = 0.0,
+                 units: Sequence[int] = (64, 16)) -> Tuple["RoutePlan", dict]:
     """The route plan for measured link rates: the uniform plan, the plan weighed by
     ``link_costs_from_rates`` (when some link is slower than the tolerance) and the direct-only
-    plan, each priced with ``RoutePlan.predicted_ms`` at the measured rates; the fastest is kept
-    (ties to the earlier candidate, in that order). Deterministic: every rank holding the same rates
-    keeps the same plan. Without rates, the uniform plan. Returns (plan, report)."""
-    uniform = RoutePlan(world, transfers, relay=relay)
+    plan, each at every ``units`` count (fewer parts per row, fewer messages), priced with
+    ``RoutePlan.predicted_ms`` at the measured rates and per-message cost; the fastest is kept
+    (ties to the earlier candidate, in that order: uniform at 64 parts first). Deterministic: every
+    rank holding the same measurements keeps the same plan. Without rates, the uniform plan at
+    ``units[0]``. Returns (plan, report)."""
+    uniform = RoutePlan(world, transfers, relay=relay, units=units[0])
     if not rates_gbps:
         return uniform, {"chosen": "uniform", "candidates": {}}
-    cands = [("uniform", uniform)]
     costs = link_costs_from_rates(rates_gbps, tolerance=tolerance)
-    if costs and len(set(costs.values())) > 1:
-        cands.append(("measured", RoutePlan(world, transfers, relay=relay, link_cost=costs)))
-    if uniform.relay:
-        cands.append(("direct", RoutePlan(world, transfers, relay=False)))
-    scored = [(p.predicted_ms(rates_gbps), i, name, p) for i, (name, p) in enumerate(cands)]
+    msg = max(0.0, float(message_us or 0.0))
+    cands = []
+    for u in units:
+        base = uniform if u == units[0] else RoutePlan(world, transfers, relay=relay, units=u)
+        tag = "" if u == units[0] else f"/{u}"
+        cands.append(("uniform" + tag, base))
+        if costs and len(set(costs.values())) > 1:
+            cands.append(("measured" + tag, RoutePlan(world, transfers, relay=relay, link_cost=costs, units=u)))
+        if base.relay:
+            cands.append(("direct" + tag, RoutePlan(world, transfers, relay=False, units=u)))
+        if msg <= 0:
+            break  # without a per-message cost, fewer parts can only lengthen the critical path
+    scored = [(p.predicted_ms(rates_gbps, message_us=msg), i, name, p) for i, (name, p) in enumerate(cands)]
     best = min(scored, key=lambda x: (round(x[0], 9), x[1]))
     return best[3], {"chosen": best[2], "candidates": {name: round(t, 4) for t, _, name, _ in scored},
+                     "message_us": round(msg, 2),
                      "slow_links": sorted(f"{a}->{b}" for (a, b), c in costs.items() if c != 16)}
 
 

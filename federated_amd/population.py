@@ -420,7 +420,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
                     window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
-                    placement_release: bool = False, link_rates=None):
+                    placement_release: bool = False, link_rates=None, message_us: float = 0.0):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -432,8 +432,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     (``placement.calibrated_stacks``: the fastest of that many allocations each, timed with the
     shard's own mix; ``info["placement"]`` holds the probe). ``link_rates``: measured per-link rates
     (GB/s, ``linkprobe.probe_links``): the route is then ``halo.choose_route``'s pick among the
-    uniform, the rate-weighted and the direct plan (``info["route_choice"]``); None = every link
-    alike."""
+    uniform, the rate-weighted and the direct plan, at 64 and (with a per-message cost
+    ``message_us`` > 0) 16 parts per row (``info["route_choice"]``); None = every link alike."""
     from .halo import choose_route, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
@@ -445,7 +445,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
-        route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates)
+        route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates, message_us=message_us)
     Pr = bounds[p + 1] - bounds[p]
     stacks, placement = None, None
     if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":

@@ -177,6 +177,25 @@ def test_choose_route_keeps_the_fastest_predicted_plan():
     assert rep["chosen"] == "uniform" and rep["candidates"] == {}
 
 
+def test_choose_route_prices_the_per_message_cost():
+    """With a large measured per-message cost, the plan with 16 parts per row (fewer messages)
+    predicts a shorter exchange than 64 parts and is kept; with none, 16 parts are not even priced
+    (they can only lengthen the byte critical path)."""
+    from federated_amd.halo import choose_route
+    tr = ring_transfers(8, 16, 4, 4, 25_000_000)
+    rates = _uniform_rates(8)
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=rates, message_us=0.0)
+    assert set(rep["candidates"]) == {"uniform", "direct"} and plan.units == 64
+    plan, rep = choose_route(8, tr, relay=True, rates_gbps=rates, message_us=200.0)
+    assert set(rep["candidates"]) == {"uniform", "direct", "uniform/16", "direct/16"}
+    assert rep["chosen"] in ("uniform/16", "direct", "direct/16") and rep["message_us"] == 200.0
+    assert rep["candidates"][rep["chosen"]] == min(rep["candidates"].values())
+    _check_plan(plan)
+    m64 = RoutePlan(8, tr, relay=True)
+    assert sum(m64.max_rank_messages(g) for g in range(len(m64.groups))) > \
+        sum(plan.max_rank_messages(g) for g in range(len(plan.groups)))
+
+
 def test_link_costs_reject_nonpositive_rates():
     from federated_amd.halo import link_costs_from_rates
     with pytest.raises(ValueError):
