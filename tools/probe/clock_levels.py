@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--pairs", type=int, default=3)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--params", type=int, default=25_000_000)
+    ap.add_argument("--carve-gib", type=int, default=0,
+                    help="carve each pair's input rows and output from allocations of this many GiB (as "
+                         "placement.calibrated_stacks does); 0 = plain allocations of the exact size")
     a = ap.parse_args()
     from federated_amd.engine import get_engine
     eng = get_engine(0)
@@ -71,9 +74,17 @@ def main():
     else:
         print(json.dumps({"metrics_error": err}), flush=True)
     pairs = []
+    hold = []
     for s in range(a.pairs):
-        ins = torch.empty((K + 1, P), device="cuda").normal_()
-        out = torch.empty(P, device="cuda")
+        if a.carve_gib:
+            big_in = torch.empty(a.carve_gib << 28, device="cuda")  # GiB of fp32
+            big_out = torch.empty(a.carve_gib << 28, device="cuda")
+            hold += [big_in, big_out]
+            ins = big_in[:(K + 1) * P].view(K + 1, P).normal_()
+            out = big_out[:P]
+        else:
+            ins = torch.empty((K + 1, P), device="cuda").normal_()
+            out = torch.empty(P, device="cuda")
         pairs.append((ins, out))
     alphas = [1.0 / (K + 1)] * K
     fns = [eng.prepare_mix_seq(out, ins[0], [ins[j] for j in range(1, K + 1)], alphas) for ins, out in pairs]
