@@ -10,7 +10,13 @@ over groups of the busiest link's load), t_tail = the boundary devices of the la
 = xGMI point-to-point rate per direction (an assumption: 50 and 64 GB/s by default), delta = the
 mixes' slowdown while RCCL copies run (measured with a stand-in: 0.10-0.16).
 
-Pure host arithmetic (no GPU). Usage: python tools/scale_model.py [--params P] [--devices D]"""
+Pure host arithmetic (no GPU). Usage: python tools/scale_model.py [--params P] [--devices D]
+
+With ``--from-lines FILE`` (bench JSON lines, one per N, e.g. the driver's SCALE record or the
+lines of `python bench.py --gpus N`), the model is re-evaluated with what each N > 1 line
+MEASURED instead of the assumptions: B_link = the line's `config.links.median_GBps`, delta and
+t_mix from its `decomposition`, T(1) from the N = 1 line's `ms_per_step`; each row prints the
+model's speed-up next to the achieved one (value / value at N = 1)."""
 import argparse
 import json
 import os
@@ -39,7 +45,12 @@ def main():
     ap.add_argument("--t-mix-ms", type=float, default=0.166, help="one K = 8 x 25M device mix on one GPU")
     ap.add_argument("--links", default="50,64", help="GB/s per xGMI link per direction (assumed)")
     ap.add_argument("--delta", default="0.10,0.16")
+    ap.add_argument("--from-lines", default=None,
+                    help="bench JSON lines (one per N): re-evaluate the model with their measured link rate, "
+                         "delta and t_mix and print it beside the achieved speed-up")
     a = ap.parse_args()
+    if a.from_lines:
+        return from_lines(a.from_lines)
     D, P, h = a.devices, a.params, a.half_window
     tmix = a.t_mix_ms * P / 25_000_000
     T1 = D * tmix
@@ -61,5 +72,56 @@ def main():
         print(json.dumps(out))
 
 
+def _lines(path):
+    out = []
+    with open(path) as fh:
+        text = fh.read()
+    try:  # a driver record: {"runs": [{"parsed": line}, ...]} or a list of lines
+        doc = json.loads(text)
+        items = doc if isinstance(doc, list) else doc.get("runs") or doc.get("results") or [doc]
+        for it in items:
+            line = it.get("parsed", it) if isinstance(it, dict) else None
+            if isinstance(line, dict) and "n_gpus" in line:
+                out.append(line)
+    except ValueError:
+        for raw in text.splitlines():
+            raw = raw.strip()
+            if raw.startswith("{"):
+                line = json.loads(raw)
+                if "n_gpus" in line:
+                    out.append(line)
+    return out
+
+
+def from_lines(path):
+    lines = sorted(_lines(path), key=lambda d: d["n_gpus"])
+    one = next((d for d in lines if d["n_gpus"] == 1), None)
+    if one is None:
+        print(json.dumps({"error": f"no N = 1 line in {path}"}))
+        return 1
+    T1, v1 = one["ms_per_step"], one["value"]
+    for d in lines:
+        if d["n_gpus"] == 1:
+            continue
+        c, dc = d.get("config", {}), d.get("decomposition") or {}
+        links = c.get("links") or {}
+        row = {"N": d["n_gpus"], "partition": c.get("partition"), "achieved_speedup": round(d["value"] / v1, 2),
+               "ms_per_step": d["ms_per_step"], "link_median_GBps": links.get("median_GBps"),
+               "delta": dc.get("delta"), "t_mix_ms": dc.get("t_mix_ms"),
+               "exchange_groups_ms": dc.get("exchange_groups_ms_sum")}
+        if dc.get("model_prediction_ms"):
+            row["model_ms"] = dc["model_prediction_ms"]
+            row["model_speedup"] = round(T1 / dc["model_prediction_ms"], 2)
+        route = c.get("halo_route") or {}
+        if links.get("median_GBps") and route.get("critical_MB") and dc.get("t_mix_ms") is not None:
+            L = c.get("devices_per_gpu") or 0
+            halo = route["critical_MB"] * 1e6 / (links["median_GBps"] * 1e9) * 1e3 + dc.get("tail_ms", 0.0)
+            comp = L * dc["t_mix_ms"] * (1 + max(0.0, dc.get("delta") or 0.0))
+            row["probe_model_ms"] = round(max(comp, halo), 4)
+            row["probe_model_speedup"] = round(T1 / max(comp, halo), 2)
+        print(json.dumps(row))
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
