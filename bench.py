@@ -95,6 +95,11 @@ def parse():
     p.add_argument("--link-probe-mb", type=float, default=64.0,
                    help="N > 1: message size (MB) of the per-link probe run before the route is planned "
                         "(federated_amd/linkprobe.py; 0 = no probe)")
+    p.add_argument("--host-lane", default="auto", choices=["auto", "off"],
+                   help="auto: probe the host lane (halo pieces over PCIe through pinned shared host memory, "
+                        "federated_amd/hostlane.py) after the link probe and offer it to the route plan; off: xGMI only")
+    p.add_argument("--lane-probe-mb", type=float, default=256.0,
+                   help="MB each rank sends over the host lane per probe round")
     p.add_argument("--no-decomposition", action="store_true",
                    help="N > 1: skip the exchange-only / compute-only sub-legs of the headline round")
     p.add_argument("--decomp-steps", type=int, default=0,
@@ -774,23 +779,29 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
         torch.cuda.synchronize()
         dist.barrier()
 
-    marks = []
+    marks, lane_marks = [], []
+    lane = routed.lane
 
     def exchange_round(record: bool):
         if not host_staged:
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(G + 1)]
             evs[0].record(comm)
-            routed.run(comm, group_done=lambda g: evs[g + 1].record(comm))
+            e0 = evs[0]
+            routed.run(comm, group_done=lambda g: evs[g + 1].record(comm), lane_timing=lane is not None)
         else:
             torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(comm)
             evs = [time.perf_counter()]
 
             def done(g):
                 torch.cuda.synchronize()
                 evs.append(time.perf_counter())
-            routed.run(comm, group_done=done)
+            routed.run(comm, group_done=done, lane_timing=lane is not None)
         if record:
             marks.append(evs)
+            if lane is not None:
+                lane_marks.append((e0, lane.last_timing))
 
     comm.wait_stream(compute)
     for _ in range(warmup):
@@ -806,6 +817,20 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     else:
         per = [[m[g].elapsed_time(m[g + 1]) for g in range(G)] for m in marks]
     group_ms = [statistics.median(col) for col in zip(*per)] if G else []
+    # the host lane (its own streams): when each group's lane pieces landed and when its copies
+    # ended, from the exchange's start (HIP events; medians over the rounds)
+    lane_arr, lane_end, lane_in, lane_out = {}, 0.0, 0.0, 0.0
+    if lane_marks:
+        arr = {}
+        ends, ins, outs = [], [], []
+        for e0, lt in lane_marks:
+            for g, e in lt["groups"].items():
+                arr.setdefault(g, []).append(e0.elapsed_time(e))
+            ends.append(max(e0.elapsed_time(lt["i1"]), e0.elapsed_time(lt["o1"])))
+            ins.append(lt["i0"].elapsed_time(lt["i1"]))
+            outs.append(lt["o0"].elapsed_time(lt["o1"]))
+        lane_arr = {g: statistics.median(v) for g, v in arr.items()}
+        lane_end, lane_in, lane_out = statistics.median(ends), statistics.median(ins), statistics.median(outs)
 
     L = shard.plan.L
     evc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -823,27 +848,55 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     delta = head_avg_ms / t_mix - 1.0 if (head_avg_ms and t_mix > 0) else 0.0
 
     schedule = shard.boundary_schedule()
+    lane_ready = None
+    if lane_arr:
+        lane_ready = []
+        for stage, _ in shard.stage_sets():
+            pos = plan.stages.index(stage)
+            got = [t for g, t in lane_arr.items() if g <= pos]
+            lane_ready.append(max(got) if got else None)
     n_int = len(shard.interior_order())
-    sim = predict_round_ms(group_ms, schedule, n_int, t_mix, max(0.0, delta))
-    x_round = sum(group_ms)
+    sim = predict_round_ms(group_ms, schedule, n_int, t_mix, max(0.0, delta), lane_ready, lane_end)
+    x_round = max(sum(group_ms), lane_end)
     tail_devices = sum(n for g, n in schedule if g >= G - 1)
     compute_bound = L * t_mix * (1.0 + max(0.0, delta))
     simple = max(compute_bound, x_round + tail_devices * t_mix)
     # max over ranks of every figure (the round ends with the slowest rank)
-    vec = torch.tensor([x_el, c_el, t_mix, delta, sim, simple, compute_bound] + group_ms, dtype=torch.float64)
+    vec = torch.tensor([x_el, c_el, t_mix, delta, sim, simple, compute_bound, lane_end, lane_in, lane_out] + group_ms,
+                       dtype=torch.float64)
     dist.all_reduce(vec, op=dist.ReduceOp.MAX)
-    x_el, c_el, t_mix, delta, sim, simple, compute_bound = vec[:7].tolist()
-    group_ms = vec[7:].tolist()
+    x_el, c_el, t_mix, delta, sim, simple, compute_bound, lane_end, lane_in, lane_out = vec[:10].tolist()
+    group_ms = vec[10:].tolist()
     x_round = sum(group_ms)
     pred = plan.predicted_group_ms(rates, message_us=message_us) if rates else [None] * G
     groups = []
     for g in range(G):
-        busiest = max(plan.group_link_elems(g).values(), default=0) * 4
+        busiest = max(plan.group_link_elems(g, lane=False).values(), default=0) * 4
         groups.append({"ms": round(group_ms[g], 4), "busiest_link_MB": round(busiest / 1e6, 2),
                        "link_GBps": round(busiest / (group_ms[g] * 1e-3) / 1e9, 2) if group_ms[g] > 0 else None,
                        "predicted_ms": round(pred[g], 4) if pred[g] is not None else None})
-    crit = plan.critical_elems() * 4
+    crit = sum(max(plan.group_link_elems(g, lane=False).values(), default=0) for g in range(G)) * 4
+    lane_rep = None
+    if lane is not None:
+        from federated_amd.halo import LANE_IN, LANE_OUT
+        lane_bytes = plan.lane_elems() * 4
+        in_b = max((n for l, n in plan.link_elems.items() if l[0] == LANE_IN), default=0) * 4
+        out_b = max((n for l, n in plan.link_elems.items() if l[1] == LANE_OUT), default=0) * 4
+        pr = None
+        if rates:
+            rin = [r for l, r in rates.items() if l[0] == LANE_IN]
+            rout = [r for l, r in rates.items() if l[1] == LANE_OUT]
+            if rin and rout:
+                pr = max(in_b / (min(rin) * 1e9), out_b / (min(rout) * 1e9)) * 1e3
+        lane_rep = {"MB_total": round(lane_bytes / 1e6, 1), "busiest_in_MB": round(in_b / 1e6, 1),
+                    "busiest_out_MB": round(out_b / 1e6, 1), "in_ms": round(lane_in, 4), "out_ms": round(lane_out, 4),
+                    "end_ms": round(lane_end, 4),
+                    "in_GBps": round(in_b / (lane_in * 1e-3) / 1e9, 2) if lane_in > 0 else None,
+                    "out_GBps": round(out_b / (lane_out * 1e-3) / 1e9, 2) if lane_out > 0 else None,
+                    "predicted_ms": round(pr, 4) if pr is not None else None,
+                    "timing": "HIP events on the lane's out / in streams, from the exchange's start"}
     return {
+        "host_lane": lane_rep,
         "steps": steps,
         "exchange_only_ms": round(x_el / steps * 1e3, 4),
         "exchange_groups_ms_sum": round(x_round, 4),
@@ -859,7 +912,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
         "compute_bound_ms": round(compute_bound, 4),
         "model_prediction_ms": round(simple, 4),
         "model_simulated_ms": round(sim, 4),
-        "bound": "exchange" if x_round + tail_devices * t_mix > compute_bound else "compute",
+        "bound": "exchange" if max(x_round, lane_end) + tail_devices * t_mix > compute_bound else "compute",
         "timing": "host clock per group (host-staged transport)" if host_staged else
                   "HIP events per exchange group on the comm stream; per-round mixes on the compute stream",
     }
@@ -974,6 +1027,40 @@ def main():
         if probe["summary"] is not None:
             probe["summary"]["wall_s"] = round(time.perf_counter() - t_probe, 2)
 
+    # The host lane (federated_amd/hostlane.py): with --route-tune links, its rates with every rank
+    # using it at once are measured after the links and join the plan's rates, so choose_route
+    # prices every plan with and without it. A token drawn by rank 0 names the shared segments.
+    lane = {"result": None, "error": None, "token": None, "opened": 0}
+    if (headline_exchanges and args.host_lane == "auto" and probe["plan_rates"] is not None
+            and args.lane_probe_mb > 0):
+        watchdog.enter("host lane probe")
+        from federated_amd.hostlane import new_token
+        from federated_amd.linkprobe import probe_lane
+        tok = [new_token() if rank == 0 else None]
+        dist.broadcast_object_list(tok, src=0)
+        lane["token"] = tok[0]
+        t_lane = time.perf_counter()
+        try:
+            lane["result"] = probe_lane(rank, world, torch.device("cuda", device), tok[0] + "p", agree_all,
+                                        elems=int(args.lane_probe_mb * 1e6 / 4))
+        except Exception as exc:
+            lane["error"] = f"{type(exc).__name__}: {exc}"
+            print(f"[bench rank {rank}] host lane probe failed: {lane['error']}", file=sys.stderr, flush=True)
+        if lane["result"] is not None:
+            lane["result"]["wall_s"] = round(time.perf_counter() - t_lane, 2)
+            probe["plan_rates"] = {**probe["plan_rates"], **lane["result"]["rates"]}
+
+    def lane_summary():
+        if args.host_lane == "off":
+            return {"mode": "off"}
+        if lane["error"] is not None:
+            return {"error": lane["error"]}
+        r = lane["result"]
+        if r is None:
+            return None
+        return {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"], "message_MB": round(r["elems"] * 4 / 1e6, 1),
+                "chunk_MB": round(r["chunk_elems"] * 4 / 2**20, 2), "timing": r["timing"], "wall_s": r.get("wall_s")}
+
     def build(partition, devices=None, relay=None):
         transport = tstate["transport"]
         shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
@@ -983,7 +1070,10 @@ def main():
                                       staged=not args.no_stages, window_batch=args.window_batch,
                                       placement_candidates=args.placement_candidates,
                                       placement_release=args.placement_release, link_rates=probe["plan_rates"],
-                                      message_us=probe["message_us"])
+                                      message_us=probe["message_us"],
+                                      lane_token=f"{lane['token']}s{lane['opened']}" if lane["token"] else None,
+                                      lane_agree=agree_all)
+        lane["opened"] += 1
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -1008,12 +1098,15 @@ def main():
         rc = xinfo.get("route_choice") or {}
         out = {"mode": route_tune, "chosen": "relayed" if plan.relay else "direct",
                "plan": rc.get("chosen", "uniform"), "candidates_predicted_ms": rc.get("candidates"),
-               "slow_links": rc.get("slow_links"), "message_us": rc.get("message_us")}
-        rates = (probe["result"] or {}).get("rates")
+               "slow_links": rc.get("slow_links"), "message_us": rc.get("message_us"),
+               "host_lane": xinfo.get("lane")}
+        rates = probe["plan_rates"] or (probe["result"] or {}).get("rates")
         if rates:
             from federated_amd.halo import RoutePlan
+            from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS
             msg = probe["message_us"]
-            out["predicted_ms"] = round(plan.predicted_ms(rates, message_us=msg), 4)
+            out["predicted_ms"] = round(plan.predicted_ms(rates, message_us=msg,
+                                                          lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4), 4)
             out["direct_predicted_ms"] = round(RoutePlan(world, plan.transfers, relay=False).predicted_ms(
                 rates, message_us=msg), 4)
         return out
@@ -1142,15 +1235,17 @@ def main():
                 "window_batch": args.window_batch,
                 "transport": tstate["transport"].name if headline_exchanges else "none (no exchange)",
                 "comparable": tstate["comparable"] if headline_exchanges else True,
-                "halo_route": ({k: route[k] for k in ("relay", "stages", "groups", "messages",
+                "halo_route": ({k: route[k] for k in ("relay", "lane", "stages", "groups", "messages",
                                                      "max_messages_per_rank_group", "link_cost")}
-                               | {"max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
+                               | {"lane_MB": round(route["lane_elems"] * 4 / 1e6, 1),
+                                  "max_link_MB": round(route["max_link_elems"] * 4 / 1e6, 1),
                                   "critical_MB": round(route["critical_elems"] * 4 / 1e6, 1),
                                   "autotune": autotune,
                                   "predicted_critical_ms": (autotune or {}).get("predicted_ms"),
                                   "achieved_critical_ms": (decomp or {}).get("exchange_groups_ms_sum")})
                 if route else None,
                 "links": probe["summary"] if probe["error"] is None else {"error": probe["error"]},
+                "host_lane": lane_summary() if headline_exchanges else None,
                 "placement": info.get("placement"),
                 "halo_carved": info.get("halo_carved"),
                 "cache_reuse": reuse,
@@ -1267,7 +1362,7 @@ def main():
             watchdog.leg("decomposition (exchange only, compute only)", seconds, decomp_expired)
             try:
                 decomp = decompose_round(shard, world, dsteps, args.warmup, avg_ms,
-                                         (probe["result"] or {}).get("rates"),
+                                         probe["plan_rates"] or (probe["result"] or {}).get("rates"),
                                          bool(getattr(tstate["transport"], "host_staged", False)),
                                          probe["message_us"])
                 decomp["achieved_ms"] = round(elapsed / args.steps * 1e3, 4)
@@ -1284,6 +1379,8 @@ def main():
             result["config"]["halo_route"]["achieved_critical_ms"] = decomp.get("exchange_groups_ms_sum")
 
     if world > 1 and not args.no_extra_legs and not weak:
+        if shard.lane is not None:
+            shard.lane.close()
         del shard
         drop_cached()
         if rank == 0:
@@ -1352,6 +1449,8 @@ def main():
                     leg["halo_carved"] = xinfo.get("halo_carved")
                 if xtune:
                     leg["autotune"] = xtune
+                if xinfo.get("lane"):
+                    leg["host_lane"] = xinfo["lane"]
                 if part != "params":
                     leg["transport"] = tstate["transport"].name
                     leg["comparable"] = tstate["comparable"]
@@ -1360,6 +1459,8 @@ def main():
                 err = f"{type(exc).__name__}: {exc}"
                 print(f"[bench rank {rank}] {name} leg failed: {err}", file=sys.stderr, flush=True)
             finally:
+                if xshard is not None and xshard.lane is not None:
+                    xshard.lane.close()
                 xshard = None
                 drop_cached()
             try:

@@ -56,6 +56,9 @@ SIGNATURES = {
     "cfa_counter_fetch": (_c_int, [_c_void_p, _c_void_p, _c_void_p]),
     "cfa_stream_signal": (_c_int, [_c_void_p, ctypes.c_uint, _c_void_p]),
     "cfa_wait_signal": (_c_int, [_c_void_p, ctypes.c_uint, _c_void_p, ctypes.c_longlong]),
+    "cfa_host_register": (_c_int, [_c_void_p, _c_size_t]),
+    "cfa_host_unregister": (_c_int, [_c_void_p]),
+    "cfa_stream_wait_word": (_c_int, [_c_void_p, ctypes.c_uint, ctypes.c_longlong, _c_void_p, _c_void_p]),
     "cfa_memcpy_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,

@@ -30,6 +30,13 @@ This module spreads the halo over every link:
   on the node), a part's weight on a link is its elements times that link's cost, so the greedy
   moves parts off slow links and the critical path is in time units; ``predicted_ms`` turns a
   plan back into milliseconds with the measured rates.
+* **Host lane** (``lane=True``, ``hostlane.py``). A third kind of path: the piece goes D2H over
+  the sender's PCIe link into shared pinned host memory and H2D over the receiver's, beside the
+  xGMI links. In the load model the lane is two pseudo-links per rank, ``(a, LANE_OUT)`` (a's D2H)
+  and ``(LANE_IN, b)`` (b's H2D), each shared by all of that rank's lane pieces; with measured
+  rates for them (``linkprobe.probe_lane``) the greedy puts on the lane what shortens the critical
+  path. Lane messages never reach the transport (``rank_ops`` leaves them out; ``lane_ops`` lists
+  them).
 * **Messages.** Each piece is one contiguous element range, so a message is one RCCL
   send/recv of a plain buffer slice. Within a group, every rank lists its sends to a peer in the
   order of one global message list, and the peer lists its receives in that same order, so the
@@ -48,6 +55,25 @@ from typing import Callable, Dict, Hashable, List, Optional, Sequence, Tuple
 
 ALIGN = 64  # elements: every piece starts 256-byte aligned (float4 kernels, RCCL copies)
 DIRECT = -1
+LANE = -2      # path id of the host lane
+LANE_OUT = -2  # pseudo endpoints of the lane in link keys: (a, LANE_OUT) is rank a's D2H,
+LANE_IN = -3   # (LANE_IN, b) is rank b's H2D
+
+
+def is_lane_link(link: Tuple[int, int]) -> bool:
+    """Is a directed link key one of the host lane's pseudo-links?"""
+    return link[0] < 0 or link[1] < 0
+
+
+def path_links(g: int, a: int, b: int, k: int) -> List[Tuple[int, int, int]]:
+    """The (group, from, to) links a piece of demand (g, a, b) loads on path k: the direct link;
+    the lane's two pseudo-links (same group: the lane streams are not ordered behind the groups);
+    or relay k's first hop in group g and second hop in group g + 1."""
+    if k == DIRECT:
+        return [(g, a, b)]
+    if k == LANE:
+        return [(g, a, LANE_OUT), (g, LANE_IN, b)]
+    return [(g, a, k), (g + 1, k, b)]
 
 
 @dataclass(frozen=True)
@@ -74,6 +100,7 @@ class Message:
     dst_key: Hashable
     dst_off: int
     count: int
+    lane: bool = False  # carried by the host lane (hostlane.py), not the transport
 
 
 def relay_key(parity: int) -> tuple:
@@ -81,8 +108,8 @@ def relay_key(parity: int) -> tuple:
 
 
 def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int = 64,
-                 relay: bool = True, cost: Optional[Dict[Tuple[int, int], int]] = None
-                 ) -> Tuple[Dict[Tuple[int, int, int], List[Tuple[int, int]]], Dict]:
+                 relay: bool = True, cost: Optional[Dict[Tuple[int, int], int]] = None,
+                 lane: bool = False) -> Tuple[Dict[Tuple[int, int, int], List[Tuple[int, int]]], Dict]:
     """Split every (group, a, b) demand over the direct link and 2-hop relays.
 
     ``demand[(g, a, b)]`` is the weight (elements) rank a sends rank b in stage position g. A
@@ -93,9 +120,10 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
     then to the lower relay rank: integer arithmetic with a fixed order, so every rank computes
     the same routes. ``cost[(a, b)]`` (positive integers, default 1 for every link) scales a
     part's weight on link a->b: with costs proportional to 1 / measured rate the loads are times.
-    Returns ``shares[(g, a, b)]`` = [(path, n_units)], path = DIRECT or the relay rank, direct
-    first then relays ascending, n_units summing to ``units``; and the link loads per group,
-    ``{(g, a, b): weight}``."""
+    ``lane`` adds the host lane (path LANE: pseudo-links (a, LANE_OUT) and (LANE_IN, b), costs
+    from ``cost`` like any link). Returns ``shares[(g, a, b)]`` = [(path, n_units)], path =
+    DIRECT, LANE or the relay rank, direct first, then the lane, then relays ascending, n_units
+    summing to ``units``; and the link loads per group, ``{(g, a, b): weight}``."""
     c = (lambda a, b: 1) if not cost else (lambda a, b: int(cost.get((a, b), 1)))
     load: Dict[Tuple[int, int, int], int] = defaultdict(int)
     gmax: Dict[int, int] = defaultdict(int)
@@ -108,21 +136,23 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
                 _, a, b = key
                 w = (demand[key] + units - 1) // units
                 best, best_cost = DIRECT, None
-                cands = [DIRECT] + ([k for k in range(world) if k != a and k != b] if relay else [])
+                cands = [DIRECT] + ([LANE] if lane else []) + \
+                    ([k for k in range(world) if k != a and k != b] if relay else [])
                 for k in cands:
-                    links = [(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]
+                    links = path_links(g, a, b, k)
                     delta = sum(max(0, load[l] + w * c(l[1], l[2]) - gmax[l[0]]) for l in links)
                     key_cost = (delta, max(load[l] + w * c(l[1], l[2]) for l in links), len(links), k)
                     if best_cost is None or key_cost < best_cost:
                         best, best_cost = k, key_cost
-                for l in ([(g, a, b)] if best == DIRECT else [(g, a, best), (g + 1, best, b)]):
+                for l in path_links(g, a, b, best):
                     load[l] += w * c(l[1], l[2])
                     gmax[l[0]] = max(gmax[l[0]], load[l])
                 counts[key][best] += 1
     shares = {}
     for key in demand:
         c = counts[key]
-        order = ([DIRECT] if c.get(DIRECT) else []) + sorted(k for k in c if k != DIRECT and c[k])
+        order = ([DIRECT] if c.get(DIRECT) else []) + ([LANE] if c.get(LANE) else []) + \
+            sorted(k for k in c if k >= 0 and c[k])
         shares[key] = [(k, c[k]) for k in order]
     return shares, dict(load)
 
@@ -134,7 +164,7 @@ def _critical(shares, demand, cost=None) -> int:
         units = sum(n for _, n in parts) or 1
         for k, n in parts:
             w = demand[(g, a, b)] * n // units
-            for l in ([(g, a, b)] if k == DIRECT else [(g, a, k), (g + 1, k, b)]):
+            for l in path_links(g, a, b, k):
                 load[l] += w * (int(cost.get((l[1], l[2]), 1)) if cost else 1)
     gmax: Dict[int, int] = defaultdict(int)
     for (g, _, _), w in load.items():
@@ -157,10 +187,12 @@ class RoutePlan:
     """The global message schedule of one routed exchange (identical on every rank)."""
 
     def __init__(self, world: int, transfers: Sequence[Transfer], relay: bool = True, units: int = 64,
-                 align: int = ALIGN, link_cost: Optional[Dict[Tuple[int, int], int]] = None):
-        """``link_cost``: integer cost per element of each directed link (``link_costs_from_rates``);
-        None = every link alike. Every rank must pass the same costs (the digest covers the
-        routes they produce)."""
+                 align: int = ALIGN, link_cost: Optional[Dict[Tuple[int, int], int]] = None,
+                 lane: bool = False):
+        """``link_cost``: integer cost per element of each directed link (``link_costs_from_rates``;
+        the lane's pseudo-links included when ``lane``); None = every link alike. ``lane`` offers
+        the host lane as a path (kept only where it shortens the critical path). Every rank must
+        pass the same costs (the digest covers the routes they produce)."""
         self.world = int(world)
         self.link_cost = {k: int(v) for k, v in link_cost.items()} if link_cost else None
         for k, v in (self.link_cost or {}).items():
@@ -177,13 +209,18 @@ class RoutePlan:
         for t in self.transfers:
             demand[(self._stage_pos[t.stage], t.src, t.dst)] += t.hi - t.lo
         self.relay = bool(relay) and world >= 3
+        self.lane = bool(lane)
         lc = self.link_cost
-        self.shares, _ = route_shares(world, dict(demand), self.units, self.relay, lc)
+        self.shares, _ = route_shares(world, dict(demand), self.units, self.relay, lc, self.lane)
         self.relay_considered = self.relay
         if self.relay:  # keep relays only where they shorten the (cost-weighted) critical path
-            direct, _ = route_shares(world, dict(demand), self.units, False, lc)
+            direct, _ = route_shares(world, dict(demand), self.units, False, lc, self.lane)
             if _critical(direct, dict(demand), lc) <= _critical(self.shares, dict(demand), lc):
                 self.relay, self.shares = False, direct
+        if self.lane:  # likewise the lane
+            nolane, _ = route_shares(world, dict(demand), self.units, self.relay, lc, False)
+            if _critical(nolane, dict(demand), lc) <= _critical(self.shares, dict(demand), lc):
+                self.lane, self.shares = False, nolane
         self.groups: List[List[Message]] = [[] for _ in range(len(self.stages) + (1 if self.relay else 0))]
         slot_use = defaultdict(int)  # (rank, stage) -> relay elements
         self.link_elems: Dict[Tuple[int, int], int] = defaultdict(int)
@@ -200,6 +237,11 @@ class RoutePlan:
                 if k == DIRECT:
                     self.groups[g].append(Message(g, t.src, t.dst, t.src_key, x0, t.dst_key, x0, cnt))
                     self.link_elems[(t.src, t.dst)] += cnt
+                    continue
+                if k == LANE:
+                    self.groups[g].append(Message(g, t.src, t.dst, t.src_key, x0, t.dst_key, x0, cnt, lane=True))
+                    self.link_elems[(t.src, LANE_OUT)] += cnt
+                    self.link_elems[(LANE_IN, t.dst)] += cnt
                     continue
                 off = slot_use[(k, t.stage)]
                 slot_use[(k, t.stage)] = off + -(-cnt // self.align) * self.align
@@ -228,17 +270,32 @@ class RoutePlan:
         return [s for s in self.stages if self.done_group(s) == group]
 
     def rank_ops(self, rank: int, group: int) -> Tuple[List[Message], List[Message]]:
-        """(sends, recvs) of ``rank`` in ``group``, each in global message order."""
-        msgs = self.groups[group]
+        """(sends, recvs) of ``rank`` in ``group`` over the transport, each in global message order
+        (host-lane messages excluded: ``lane_ops``)."""
+        msgs = [m for m in self.groups[group] if not m.lane]
         return [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank]
+
+    def lane_ops(self, rank: int) -> Tuple[List[Message], List[Message]]:
+        """(sends, recvs) of ``rank`` over the host lane, every group, in global message order."""
+        msgs = [m for g in self.groups for m in g if m.lane]
+        return [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank]
+
+    def lane_elems(self) -> int:
+        return sum(m.count for g in self.groups for m in g if m.lane)
 
     def max_link_elems(self) -> int:
         return max(self.link_elems.values(), default=0)
 
-    def group_link_elems(self, group: int) -> Dict[Tuple[int, int], int]:
+    def group_link_elems(self, group: int, lane: bool = True) -> Dict[Tuple[int, int], int]:
+        """Elements per directed link in ``group``; the lane's pseudo-links included unless
+        ``lane`` is False (the xGMI links alone)."""
         load: Dict[Tuple[int, int], int] = defaultdict(int)
         for m in self.groups[group]:
-            load[(m.src, m.dst)] += m.count
+            if not m.lane:
+                load[(m.src, m.dst)] += m.count
+            elif lane:
+                load[(m.src, LANE_OUT)] += m.count
+                load[(LANE_IN, m.dst)] += m.count
         return dict(load)
 
     def critical_elems(self) -> int:
@@ -257,10 +314,13 @@ class RoutePlan:
         return total
 
     def max_rank_messages(self, group: int) -> int:
-        """The most messages one rank issues in one direction (sends or receives) in ``group``."""
+        """The most transport messages one rank issues in one direction (sends or receives) in
+        ``group``."""
         sends: Dict[int, int] = defaultdict(int)
         recvs: Dict[int, int] = defaultdict(int)
         for m in self.groups[group]:
+            if m.lane:
+                continue
             sends[m.src] += 1
             recvs[m.dst] += 1
         return max(list(sends.values()) + list(recvs.values()), default=0)
@@ -268,10 +328,10 @@ class RoutePlan:
     def predicted_group_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4,
                            message_us: float = 0.0) -> List[float]:
         """Per group, the time its slowest link needs at the given per-direction rates (GB/s; a link
-        missing from ``rates_gbps`` takes the slowest rate given), plus ``message_us`` per message
-        of the rank that issues the most in the group (the per-message cost the link probe
-        measures): the group's length when every link runs at its measured rate and the groups run
-        back to back."""
+        missing from ``rates_gbps`` takes the slowest rate given; the lane's pseudo-links take
+        their probed rates), plus ``message_us`` per message of the rank that issues the most in the
+        group (the per-message cost the link probe measures): the group's length when every link
+        runs at its measured rate and the groups run back to back."""
         slow = min(rates_gbps.values()) if rates_gbps else None
         out = []
         for g in range(len(self.groups)):
@@ -286,8 +346,15 @@ class RoutePlan:
         return out
 
     def predicted_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4,
-                     message_us: float = 0.0) -> float:
-        return sum(self.predicted_group_ms(rates_gbps, elem_bytes, message_us))
+                     message_us: float = 0.0, lane_chunk_bytes: int = 0) -> float:
+        """Sum of ``predicted_group_ms``; with lane messages, plus the lane pipeline's fill: one
+        ``lane_chunk_bytes`` chunk D2H before the first H2D can start, at the slowest lane rate."""
+        t = sum(self.predicted_group_ms(rates_gbps, elem_bytes, message_us))
+        if lane_chunk_bytes and any(m.lane for g in self.groups for m in g):
+            lane_rates = [r for l, r in rates_gbps.items() if is_lane_link(l) and r > 0]
+            if lane_rates:
+                t += lane_chunk_bytes / (min(lane_rates) * 1e9) * 1e3
+        return t
 
     def digest(self) -> str:
         h = hashlib.sha1()
@@ -307,6 +374,8 @@ class RoutePlan:
             "max_link_elems": self.max_link_elems(),
             "critical_elems": self.critical_elems(),
             "link_cost": "measured" if self.link_cost else "uniform",
+            "lane": self.lane,
+            "lane_elems": self.lane_elems(),
         }
 
 
@@ -316,14 +385,23 @@ class RoutedExchange:
     ``buffers(key)`` returns the rank's 1-D tensor for a bucket key (the element ranges of the
     plan index into it). Relay staging is allocated here. ``run`` issues the groups in order on
     ``stream`` and calls ``stage_done(stage)`` right after the group that completes each stage,
-    so the caller can record an event there and start that stage's boundary mixes."""
+    so the caller can record an event there and start that stage's boundary mixes. A plan with
+    host-lane messages needs ``lane`` (a ``hostlane.HostLane`` opened on the same plan): ``run``
+    issues its copies first, on the lane's own streams, and ``lane_event(stage)`` is the event
+    after which the lane's pieces of that stage (and every earlier one) have landed."""
 
     def __init__(self, plan: RoutePlan, rank: int, buffers: Callable[[Hashable], "object"], transport,
-                 device=None, dtype=None, relay=None):
+                 device=None, dtype=None, relay=None, lane=None):
         """``relay``: caller-provided staging of shape ``[2, >= slot_elems(rank)]`` (e.g. carved from
         a calibrated allocation); allocated here when None."""
         import torch
         self.plan, self.rank, self.transport = plan, int(rank), transport
+        ls, lr = plan.lane_ops(self.rank)
+        if (ls or lr) and lane is None:
+            raise ValueError(f"rank {rank}: the plan sends {len(ls)} / receives {len(lr)} pieces over the host lane "
+                             "but no lane was opened (population.RingPopulationShard.open_lane)")
+        self.lane = lane
+        self._lane_events = {}
         n = plan.slot_elems(self.rank)
         if relay is not None:
             if relay.dim() != 2 or relay.shape[0] != 2 or relay.shape[1] < n:
@@ -345,10 +423,22 @@ class RoutedExchange:
             self.ops.append(prep(s, r) if prep is not None else (s, r))
         self.done = [plan.stages_done_after(g) for g in range(len(plan.groups))]
 
+    def lane_event(self, stage: int):
+        """The last lane event at or before ``stage``'s group (None: nothing of it on the lane)."""
+        pos = self.plan.stages.index(stage)
+        best = None
+        for g, e in self._lane_events.items():
+            if g <= pos and (best is None or g > best[0]):
+                best = (g, e)
+        return best[1] if best else None
+
     def run(self, stream=None, stage_done: Optional[Callable[[int], None]] = None,
-            group_done: Optional[Callable[[int], None]] = None) -> None:
+            group_done: Optional[Callable[[int], None]] = None, lane_timing: bool = False) -> None:
         """Issue every group in order; ``group_done(g)`` (optional) right after group g is issued
-        (the bench's exchange-only timing records an event there)."""
+        (the bench's exchange-only timing records an event there). The host lane's copies go first,
+        on its own streams after ``stream``'s earlier work (``lane_timing``: with HIP events)."""
+        if self.lane is not None:
+            self._lane_events = self.lane.run(stream, timing=lane_timing)
         for g, op in enumerate(self.ops):
             if callable(op):
                 op(stream)
@@ -382,38 +472,57 @@ def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int =
     return out
 
 
+def _link_name(link: Tuple[int, int]) -> str:
+    a, b = link
+    if b == LANE_OUT:
+        return f"{a}->host"
+    if a == LANE_IN:
+        return f"host->{b}"
+    return f"{a}->{b}"
+
+
 def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
                  rates_gbps: Optional[Dict[Tuple[int, int], float]] = None,
                  tolerance: float = 0.15, message_us: float = 0.0,
-                 units: Sequence[int] = (64, 16)) -> Tuple["RoutePlan", dict]:
+                 units: Sequence[int] = (64, 16), lane_chunk_bytes: int = 0) -> Tuple["RoutePlan", dict]:
     """The route plan for measured link rates: the uniform plan, the plan weighed by
     ``link_costs_from_rates`` (when some link is slower than the tolerance) and the direct-only
     plan, each at every ``units`` count (fewer parts per row, fewer messages), priced with
     ``RoutePlan.predicted_ms`` at the measured rates and per-message cost; the fastest is kept
-    (ties to the earlier candidate, in that order: uniform at 64 parts first). Deterministic: every
-    rank holding the same measurements keeps the same plan. Without rates, the uniform plan at
-    ``units[0]``. Returns (plan, report)."""
+    (ties to the earlier candidate, in that order: uniform at 64 parts first). When
+    ``rates_gbps`` also holds the host lane's pseudo-links (``linkprobe.probe_lane``) every
+    candidate is offered again with the lane (``+lane``, priced with the lane pipeline's fill of
+    one ``lane_chunk_bytes`` chunk), after the lane-free ones. Deterministic: every rank holding
+    the same measurements keeps the same plan. Without rates, the uniform plan at ``units[0]``
+    without the lane. Returns (plan, report)."""
     uniform = RoutePlan(world, transfers, relay=relay, units=units[0])
     if not rates_gbps:
         return uniform, {"chosen": "uniform", "candidates": {}}
+    lane_ok = any(is_lane_link(l) for l in rates_gbps)
+    xgmi = {l: r for l, r in rates_gbps.items() if not is_lane_link(l)}
     costs = link_costs_from_rates(rates_gbps, tolerance=tolerance)
     msg = max(0.0, float(message_us or 0.0))
     cands = []
-    for u in units:
-        base = uniform if u == units[0] else RoutePlan(world, transfers, relay=relay, units=u)
-        tag = "" if u == units[0] else f"/{u}"
-        cands.append(("uniform" + tag, base))
-        if costs and len(set(costs.values())) > 1:
-            cands.append(("measured" + tag, RoutePlan(world, transfers, relay=relay, link_cost=costs, units=u)))
-        if base.relay:
-            cands.append(("direct" + tag, RoutePlan(world, transfers, relay=False, units=u)))
-        if msg <= 0:
-            break  # without a per-message cost, fewer parts can only lengthen the critical path
-    scored = [(p.predicted_ms(rates_gbps, message_us=msg), i, name, p) for i, (name, p) in enumerate(cands)]
+    for lane in ([False, True] if lane_ok else [False]):
+        sfx = "+lane" if lane else ""
+        for u in units:
+            base = uniform if (u == units[0] and not lane) else \
+                RoutePlan(world, transfers, relay=relay, units=u, lane=lane)
+            tag = ("" if u == units[0] else f"/{u}") + sfx
+            cands.append(("uniform" + tag, base))
+            if costs and len(set(costs.values())) > 1:
+                cands.append(("measured" + tag, RoutePlan(world, transfers, relay=relay, link_cost=costs, units=u,
+                                                         lane=lane)))
+            if base.relay:
+                cands.append(("direct" + tag, RoutePlan(world, transfers, relay=False, units=u, lane=lane)))
+            if msg <= 0:
+                break  # without a per-message cost, fewer parts can only lengthen the critical path
+    scored = [(p.predicted_ms(rates_gbps, message_us=msg, lane_chunk_bytes=lane_chunk_bytes), i, name, p)
+              for i, (name, p) in enumerate(cands)]
     best = min(scored, key=lambda x: (round(x[0], 9), x[1]))
     return best[3], {"chosen": best[2], "candidates": {name: round(t, 4) for t, _, name, _ in scored},
-                     "message_us": round(msg, 2),
-                     "slow_links": sorted(f"{a}->{b}" for (a, b), c in costs.items() if c != 16)}
+                     "message_us": round(msg, 2), "lane_offered": lane_ok,
+                     "slow_links": sorted(_link_name(l) for l, c in costs.items() if c != 16 and l in xgmi)}
 
 
 def ring_transfers(dev_world: int, L: int, hl: int, hr: int, P: int, slice_world: int = 1,

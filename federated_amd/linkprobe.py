@@ -196,3 +196,97 @@ def min_rate(probe: Optional[dict]) -> Optional[float]:
     if not probe or not probe.get("rates"):
         return None
     return min(probe["rates"].values())
+
+
+def agree_gloo(ok: bool, group=None) -> bool:
+    """All-ranks AND over the control plane (a gloo all-reduce MIN): also a barrier."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elems: int = 64 << 20, reps: int = 3,
+               warmup: int = 1, chunk_elems: Optional[int] = None, timeout_s: float = 60.0) -> dict:
+    """The host lane's rates (``hostlane.py``) with every rank using it at once: rank a sends
+    ``elems`` floats to rank a + 1 and receives as many from rank a - 1 over pinned shared host
+    memory, D2H and H2D pipelined in chunks, ``reps`` timed rounds after ``warmup``: at world 2 the
+    exact pattern of the N = 2 halo, and at any world every GPU's PCIe link busy in both
+    directions while host memory serves all of them. Per rank: the out rate (its D2H stream's
+    bytes / time) and the in rate (bytes / time from the in stream's start to its last H2D: the
+    pipelined lane end to end), medians over the reps, HIP events on the lane's streams (host
+    clock on CPU tensors). Collective (``agree(ok)``: the control plane's all-ranks AND; a failure
+    on any rank raises on every rank). Returns {"rates":
+    {(a, LANE_OUT): GB/s, (LANE_IN, b): GB/s}, "out_GBps": [per rank], "in_GBps": [per rank],
+    "elems": elems, "chunk_elems": c}, identical on every rank (all-reduced)."""
+    import statistics
+    import torch
+    import torch.distributed as dist
+    from .halo import LANE_IN, LANE_OUT, Message
+    from .hostlane import DEFAULT_CHUNK_ELEMS, HostLane
+
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    elems = max(ALIGN, elems // ALIGN * ALIGN)
+    bufs = {"send": torch.full((elems,), float(rank), dtype=torch.float32, device=dev),
+            "recv": torch.empty(elems, dtype=torch.float32, device=dev)}
+    msgs = [Message(0, a, (a + 1) % world, "send", 0, "recv", 0, elems, lane=True) for a in range(world)]
+    lane = HostLane.open(rank, [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank],
+                         lambda k: bufs[k], dev, token, agree, chunk_elems=chunk_elems or DEFAULT_CHUNK_ELEMS,
+                         timeout_s=timeout_s)
+    gpu = dev.type == "cuda"
+    stream = torch.cuda.Stream(dev) if gpu else None
+    outs, ins, err = [], [], None
+    try:
+        for _ in range(warmup):
+            lane.run(stream)
+        if gpu:
+            torch.cuda.synchronize(dev)
+        lane.check()
+    except Exception as exc:
+        err = f"{type(exc).__name__}: {exc}"
+    if agree(err is None):
+        try:
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                lane.run(stream, timing=gpu)
+                if gpu:
+                    torch.cuda.synchronize(dev)
+                    tm = lane.timing_ms()
+                    outs.append(tm["out_ms"])
+                    ins.append(tm["in_ms"])
+                else:
+                    dt = (time.perf_counter() - t0) * 1e3
+                    outs.append(dt)
+                    ins.append(dt)
+                lane.check()
+            src = (rank - 1) % world
+            got = (float(bufs["recv"][0].item()), float(bufs["recv"][-1].item()))
+            if got != (float(src), float(src)):
+                raise RuntimeError(f"lane probe: rank {rank} received {got}, not rank {src}'s rows")
+        except Exception as exc:
+            err = f"{type(exc).__name__}: {exc}"
+    else:
+        err = err or "the warm-up failed on another rank"
+    lane.close()
+    if not agree(err is None):
+        raise RuntimeError(f"lane probe: {err or 'failed on another rank'}")
+    t = torch.zeros((2, world), dtype=torch.float64)
+    t[0, rank] = statistics.median(outs)
+    t[1, rank] = statistics.median(ins)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    nbytes = elems * 4
+    out_r = [nbytes / (float(x) * 1e-3) / 1e9 if x > 0 else 0.0 for x in t[0].tolist()]
+    in_r = [nbytes / (float(x) * 1e-3) / 1e9 if x > 0 else 0.0 for x in t[1].tolist()]
+    rates = {}
+    for a in range(world):
+        if out_r[a] > 0:
+            rates[(a, LANE_OUT)] = out_r[a]
+        if in_r[a] > 0:
+            rates[(LANE_IN, a)] = in_r[a]
+    del bufs
+    return {"rates": rates, "out_GBps": [round(x, 2) for x in out_r], "in_GBps": [round(x, 2) for x in in_r],
+            "elems": elems, "chunk_elems": lane.chunk_elems,
+            "timing": "HIP events on the lane streams" if gpu else "host clock (CPU tensors)"}

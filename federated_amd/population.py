@@ -222,6 +222,7 @@ class RingPopulationShard:
         self.alphas = [1.0 / (plan.K + 1)] * plan.K
         self._route_plan = route
         self._routed = None
+        self.lane = None  # hostlane.HostLane, when the route puts pieces on the host lane (open_lane)
         # order of the interior mixes within a round (None: ascending device id, the ring order);
         # the mixes write a separate stack, so any order gives the same round
         self.mix_order: Optional[List[int]] = None
@@ -265,8 +266,20 @@ class RingPopulationShard:
         if self._routed is None and self._route_plan is not None:
             from .halo import RoutedExchange
             self._routed = RoutedExchange(self._route_plan, self.rank, self.buffer, self.transport,
-                                          self.device, self.models.dtype, relay=self._relay_buf)
+                                          self.device, self.models.dtype, relay=self._relay_buf, lane=self.lane)
         return self._routed
+
+    def open_lane(self, token: str, agree, **kw) -> None:
+        """Open the host lane of the route (collective: every rank of the plan calls it with the
+        same ``token``; ``agree(ok)`` is the control plane's all-ranks AND). A no-op for a route
+        without lane pieces anywhere."""
+        route = self._route_plan
+        if route is None or not route.lane:
+            return
+        from .hostlane import HostLane
+        sends, recvs = route.lane_ops(self.rank)
+        self.lane = HostLane.open(self.rank, sends, recvs, self.buffer, self.device, token, agree, **kw)
+        self._routed = None
 
     def exchange(self, stream=None) -> None:
         """The whole halo exchange, issued on ``stream`` (synchronous for host transports)."""
@@ -378,9 +391,14 @@ class RingPopulationShard:
                 cs.wait_event(ev)
             elif ms is not cs:
                 cs.wait_stream(ms)
+            lev = routed.lane_event(stage) if routed.lane is not None else None
+            if lev is not None:
+                cs.wait_event(lev)
             self._mix_set(devs, cs)
         if ms is not cs:
             cs.wait_stream(ms)  # the next round's exchange must not overwrite a halo still read
+        if routed.lane is not None and on_gpu:
+            routed.lane.wait_streams(cs)  # nor the lane's; and the rows have left before they change
 
     @property
     def bytes_per_round(self) -> int:
@@ -389,19 +407,24 @@ class RingPopulationShard:
 
 
 def predict_round_ms(group_ms: List[float], schedule: List[Tuple[int, int]], n_interior: int, t_mix_ms: float,
-                     delta: float) -> float:
+                     delta: float, lane_ready_ms: Optional[List[Optional[float]]] = None,
+                     lane_end_ms: float = 0.0) -> float:
     """Length of one overlapped round from its measured parts (the bench's N > 1 decomposition):
     the exchange groups run back to back from t = 0 on the comm stream (``group_ms``, measured
     with no mixes); the compute stream mixes the ``n_interior`` interior devices from t = 0, then
     each boundary set of ``schedule`` [(group, devices)] once its group has landed. A mix takes
     ``t_mix_ms`` (measured with no exchange) stretched by (1 + ``delta``) while the exchange is
     still running (RCCL's copy kernels share the CUs and HBM; ``delta`` measured from the
-    headline's own interior mixes), ``t_mix_ms`` after it."""
+    headline's own interior mixes), ``t_mix_ms`` after it. With the host lane,
+    ``lane_ready_ms[i]`` (per schedule entry, None = nothing of it on the lane) is when the lane's
+    pieces of that boundary set have landed (measured from the exchange's start) and
+    ``lane_end_ms`` when the lane's last copy ends: a set waits for both paths, and the exchange
+    lasts until both are done."""
     ends, t = [], 0.0
     for g in group_ms:
         t += g
         ends.append(t)
-    t_x = ends[-1] if ends else 0.0
+    t_x = max(ends[-1] if ends else 0.0, lane_end_ms)
 
     def mixes(n, t):
         for _ in range(n):
@@ -409,9 +432,11 @@ def predict_round_ms(group_ms: List[float], schedule: List[Tuple[int, int]], n_i
         return t
 
     t = mixes(n_interior, 0.0)
-    for g, n in schedule:
+    for i, (g, n) in enumerate(schedule):
         if ends:
             t = max(t, ends[min(g, len(ends) - 1)])
+        if lane_ready_ms and i < len(lane_ready_ms) and lane_ready_ms[i] is not None:
+            t = max(t, lane_ready_ms[i])
         t = mixes(n, t)
     return max(t, t_x)
 
@@ -420,7 +445,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                     transport=None, engine=None, partition: str = "devices",
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
                     window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
-                    placement_release: bool = False, link_rates=None, message_us: float = 0.0):
+                    placement_release: bool = False, link_rates=None, message_us: float = 0.0,
+                    lane_token: Optional[str] = None, lane_agree=None, lane_chunk_elems: Optional[int] = None):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -433,7 +459,11 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     shard's own mix; ``info["placement"]`` holds the probe). ``link_rates``: measured per-link rates
     (GB/s, ``linkprobe.probe_links``): the route is then ``halo.choose_route``'s pick among the
     uniform, the rate-weighted and the direct plan, at 64 and (with a per-message cost
-    ``message_us`` > 0) 16 parts per row (``info["route_choice"]``); None = every link alike."""
+    ``message_us`` > 0) 16 parts per row (``info["route_choice"]``); None = every link alike.
+    When ``link_rates`` also holds the host lane's pseudo-links (``linkprobe.probe_lane``) the lane
+    is offered to the route too; if the chosen route uses it the shard's lane is opened here
+    (collective: every rank passes the same ``lane_token`` and ``lane_agree``, the control plane's
+    all-ranks AND)."""
     from .halo import choose_route, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
@@ -445,7 +475,12 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
-        route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates, message_us=message_us)
+        from .hostlane import DEFAULT_CHUNK_ELEMS
+        chunk = int(lane_chunk_elems or DEFAULT_CHUNK_ELEMS)
+        route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates, message_us=message_us,
+                                           lane_chunk_bytes=chunk * 4)
+        if route.lane and (lane_token is None or lane_agree is None):
+            raise ValueError("the chosen route uses the host lane: make_ring_shard needs lane_token and lane_agree")
     Pr = bounds[p + 1] - bounds[p]
     stacks, placement = None, None
     if placement_candidates > 1 and engine is not None and torch.device(device).type == "cuda":
@@ -455,6 +490,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         stacks = (models, mixed)
     shard = RingPopulationShard(plan, Pr, device, transport, engine, dtype, window_batch, route=route, rank=rank,
                                 stacks=stacks, carve=stacks is not None)
+    if route is not None and route.lane:
+        shard.open_lane(lane_token, lane_agree, chunk_elems=chunk)
     info = {"partition": partition, "device_groups": gd, "param_slices": gp,
             "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L,
             "placement": placement, "halo_carved": shard.carved}
@@ -462,4 +499,6 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         info["route"] = route.summary()
         info["route_digest"] = route.digest()
         info["route_choice"] = route_choice
+        if shard.lane is not None:
+            info["lane"] = shard.lane.summary()
     return shard, info

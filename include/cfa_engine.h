@@ -249,6 +249,21 @@ CFA_API int cfa_counter_fetch(unsigned long long* counter, unsigned long long* h
 CFA_API int cfa_stream_signal(unsigned* word_dev, unsigned value, void* stream);
 CFA_API int cfa_wait_signal(const unsigned* word_host, unsigned value, void* stream, long long spin_us);
 
+/* Host lane of the routed halo (federated_amd/hostlane.py): part of a round's halo travels
+ * D2H over the sender's PCIe link into shared pinned host memory and H2D over the receiver's,
+ * beside the xGMI links. cfa_host_register / cfa_host_unregister pin (hipHostRegister, mapped and
+ * portable) and release a caller-mapped host range, e.g. a shared-memory segment both ranks map.
+ * cfa_stream_wait_word enqueues a one-lane kernel that polls the 32-bit word at `word_dev` (device
+ * address of a pinned host word the other rank's stream raises with cfa_stream_signal) until it
+ * reaches `value` in sequence order ((int)(word - value) >= 0); the stream's later work waits for
+ * it. After `timeout_us` without it the kernel stores `value` into `status_dev` and exits, so no
+ * wave spins forever: the caller checks the status word after the round. A wait that finds the
+ * status word already set returns at once (one timeout per status word, not one per wait). */
+CFA_API int cfa_host_register(void* host, size_t bytes);
+CFA_API int cfa_host_unregister(void* host);
+CFA_API int cfa_stream_wait_word(const unsigned* word_dev, unsigned value, long long timeout_us,
+                                 unsigned* status_dev, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.
  *   out[i] = fold_j( w <- w + alphas[j] * (nbrs[j][i] - w) ), w0 = local[i]

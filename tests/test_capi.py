@@ -103,6 +103,28 @@ def test_wait_signal_sees_a_word_set_by_another_thread_without_gpu():
         _lib.call("cfa_stream_signal", None, 1, None)
 
 
+def test_host_lane_entry_points_validate_before_any_hip_call():
+    """The host lane's C-ABI refuses null words / ranges and a non-positive timeout before it
+    touches HIP (no GPU here)."""
+    import ctypes
+
+    from federated_amd import _lib
+    word = (ctypes.c_uint * 2)(0, 0)
+    addr = ctypes.addressof(word)
+    with pytest.raises(_lib.CFAError, match="null wait or status word"):
+        _lib.call("cfa_stream_wait_word", None, 1, 1000, addr, None)
+    with pytest.raises(_lib.CFAError, match="null wait or status word"):
+        _lib.call("cfa_stream_wait_word", addr, 1, 1000, None, None)
+    with pytest.raises(_lib.CFAError, match="timeout_us must be positive"):
+        _lib.call("cfa_stream_wait_word", addr, 1, 0, addr + 4, None)
+    with pytest.raises(_lib.CFAError, match="null or empty host range"):
+        _lib.call("cfa_host_register", None, 4096)
+    with pytest.raises(_lib.CFAError, match="null or empty host range"):
+        _lib.call("cfa_host_register", addr, 0)
+    with pytest.raises(_lib.CFAError, match="null host pointer"):
+        _lib.call("cfa_host_unregister", None)
+
+
 def test_single_hip_runtime_in_process():
     """libcfa must bind to the HIP runtime torch loaded (one libamdhip64 mapped)."""
     import torch  # noqa: F401

@@ -41,7 +41,7 @@ def test_bench_line_contract():
 N_GT_1_FIELDS = [("value", float), ("ms_per_step", float), ("n_gpus", int), ("exit_status", int),
                  ("config", dict), ("roofline", dict), ("partitions", dict)]
 CONFIG_FIELDS = ["partition", "transport", "comparable", "rccl_version", "halo_route", "cache_reuse", "rows_note",
-                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback", "links", "rccl_log"]
+                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback", "links", "rccl_log", "host_lane"]
 
 
 def _self_launched(extra, timeout=240):
@@ -76,8 +76,16 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     links = c["links"]
     assert links["rates_GBps"][0][1] > 0 and links["rates_GBps"][1][0] > 0 and links["rates_GBps"][0][0] is None
     at = c["halo_route"]["autotune"]
-    assert at["mode"] == "links" and at["plan"] in ("uniform", "measured", "direct") and at["predicted_ms"] > 0
+    assert at["mode"] == "links" and at["predicted_ms"] > 0
+    assert at["plan"].split("+")[0] in ("uniform", "measured", "direct")
     assert at["candidates_predicted_ms"]["uniform"] > 0 and c["halo_route"]["link_cost"] in ("uniform", "measured")
+    # the host lane: probed with both ranks on it at once, offered to the plan, reported when used
+    hl = c["host_lane"]
+    assert len(hl["out_GBps"]) == 2 and min(hl["out_GBps"] + hl["in_GBps"]) > 0
+    assert "uniform+lane" in at["candidates_predicted_ms"]
+    if at["plan"].endswith("+lane"):
+        assert c["halo_route"]["lane"] and c["halo_route"]["lane_MB"] > 0 and at["host_lane"]["in_MB"] > 0
+        assert d["decomposition"]["host_lane"]["in_ms"] > 0 and d["decomposition"]["host_lane"]["end_ms"] > 0
     dc = d["decomposition"]
     for key in ("exchange_only_ms", "exchange_groups_ms_sum", "exchange_link_GBps", "exchange_groups",
                 "compute_only_ms", "t_mix_ms", "delta", "tail_ms", "model_prediction_ms", "model_simulated_ms",

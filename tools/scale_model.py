@@ -8,7 +8,10 @@ L = devices per rank (x the element slice for params / hybrid), t_mix = one devi
 GPU (measured: 0.166 ms for K = 8 x 25M), C_halo = RoutePlan.critical_elems * 4 bytes (the sum
 over groups of the busiest link's load), t_tail = the boundary devices of the last stage, B_link
 = xGMI point-to-point rate per direction (an assumption: 50 and 64 GB/s by default), delta = the
-mixes' slowdown while RCCL copies run (measured with a stand-in: 0.10-0.16).
+mixes' slowdown while RCCL copies run (measured with a stand-in: 0.10-0.16). With ``--lane``
+rates > 0 the halo may also take the host lane (federated_amd/hostlane.py: PCIe through pinned
+host memory, that rate per GPU and direction): the plan is then ``halo.choose_route``'s pick at
+those rates and C_halo / B_link becomes its predicted exchange time (for lane 0 the two agree).
 
 Pure host arithmetic (no GPU). Usage: python tools/scale_model.py [--params P] [--devices D]
 
@@ -37,6 +40,23 @@ def critical_bytes(world, partition, D, h, P, groups=None, relay=True):
     return plan.critical_elems() * 4, plan.relay
 
 
+def exchange_ms(world, partition, D, h, P, link_gbps, lane_gbps, groups=None):
+    """The chosen plan's predicted exchange time at uniform link rates plus (lane_gbps > 0) the
+    host lane's, and the MB it puts on the lane."""
+    from federated_amd.halo import LANE_IN, LANE_OUT, choose_route
+    from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS
+    gd, gp = partition_shape(partition, world, D, groups)
+    if gd < 2:
+        return 0.0, 0.0
+    tr = ring_transfers(gd, D // gd, h, h, P, slice_world=gp, slice_bounds=slice_bounds(P, gp))
+    rates = {(a, b): link_gbps for a in range(world) for b in range(world) if a != b}
+    if lane_gbps > 0:
+        rates.update({(a, LANE_OUT): lane_gbps for a in range(world)})
+        rates.update({(LANE_IN, a): lane_gbps for a in range(world)})
+    plan, _ = choose_route(world, tr, rates_gbps=rates, lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4)
+    return plan.predicted_ms(rates, lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4), plan.lane_elems() * 4 / 1e6
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--params", type=int, default=25_000_000)
@@ -45,6 +65,7 @@ def main():
     ap.add_argument("--t-mix-ms", type=float, default=0.166, help="one K = 8 x 25M device mix on one GPU")
     ap.add_argument("--links", default="50,64", help="GB/s per xGMI link per direction (assumed)")
     ap.add_argument("--delta", default="0.10,0.16")
+    ap.add_argument("--lane", default="0", help="GB/s of the host lane per GPU and direction (0 = xGMI only)")
     ap.add_argument("--from-lines", default=None,
                     help="bench JSON lines (one per N): re-evaluate the model with their measured link rate, "
                          "delta and t_mix and print it beside the achieved speed-up")
@@ -56,6 +77,7 @@ def main():
     T1 = D * tmix
     links = [float(x) for x in a.links.split(",")]
     deltas = [float(x) for x in a.delta.split(",")]
+    lanes = [float(x) for x in a.lane.split(",")]
     rows = [(2, "devices", None), (4, "devices", None), (4, "hybrid", 2), (8, "devices", None),
             (8, "hybrid", 4), (8, "hybrid", 2), (2, "params", None), (4, "params", None), (8, "params", None)]
     for N, part, g in rows:
@@ -65,10 +87,16 @@ def main():
         out = {"N": N, "partition": part + (f" G={g}" if g else ""), "relayed": relayed,
                "mixes_per_rank_ms": round(mixes, 2), "critical_halo_MB": round(crit / 1e6, 1)}
         for bl in links:
-            for dl in deltas:
-                halo = crit / (bl * 1e9) * 1e3 + (2 * tmix / gp if crit else 0.0)
-                T = max(mixes * (1 + (dl if crit else 0.0)), halo)  # no exchange, no RCCL kernels
-                out[f"speedup@{bl:g}GBps,delta{dl:g}"] = round(T1 / T, 2)
+            for ln in lanes:
+                x_ms, lane_mb = (crit / (bl * 1e9) * 1e3, 0.0) if ln <= 0 else \
+                    exchange_ms(N, part, D, h, P, bl, ln, g)
+                tag = f"{bl:g}GBps" + (f",lane{ln:g}" if ln > 0 else "")
+                if ln > 0:
+                    out[f"lane_MB@{tag}"] = round(lane_mb, 1)
+                for dl in deltas:
+                    halo = x_ms + (2 * tmix / gp if crit else 0.0)
+                    T = max(mixes * (1 + (dl if crit else 0.0)), halo)  # no exchange, no RCCL kernels
+                    out[f"speedup@{tag},delta{dl:g}"] = round(T1 / T, 2)
         print(json.dumps(out))
 
 
