@@ -149,6 +149,7 @@ def _worker(rank, world, port, D, P, rounds, q):
                                       link_rates=rates, lane_token=tok[0], lane_agree=agree_gloo,
                                       lane_chunk_elems=256)
         ok &= bool(info["route"]["lane"]) and "+lane" in info["route_choice"]["chosen"]
+        ok &= bool(info["route"]["relay"]) == (world == 8)  # at 8 ranks relays and the lane together
         agree_gloo(True)  # every rank has unlinked the names it created
         ok &= not [f for f in os.listdir("/dev/shm") if tok[0] in f]
         plan = shard.plan
@@ -172,7 +173,7 @@ def _worker(rank, world, port, D, P, rounds, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,D", [(2, 16), (4, 16)])
+@pytest.mark.parametrize("world,D", [(2, 16), (4, 16), (8, 64)])
 def test_host_lane_rounds_gloo(world, D):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
