@@ -316,6 +316,9 @@ class HostLane:
             seq = (r * self._in_n[src_rank] + k + 1) & 0xFFFFFFFF
             _lib.check("cfa_stream_wait_word", lib.cfa_stream_wait_word(
                 ctypes.c_void_p(seg.word_dev(READY)), seq, tmo, ctypes.c_void_p(self._status_dev + 4), ish))
+            if timing and i == 0:  # the first chunk has landed in host memory: the pipeline is full
+                ev["i_first"] = torch.cuda.Event(enable_timing=True)
+                ev["i_first"].record(is_)
             _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(ctypes.c_void_p(dst.data_ptr()),
                                                                ctypes.c_void_p(seg.host_ptr(par, so)), dst.numel() * 4,
                                                                ish))
@@ -336,12 +339,17 @@ class HostLane:
 
     def timing_ms(self) -> Optional[dict]:
         """After the stream has been synchronised: the last timed round's out-stream and
-        in-stream milliseconds and each group's arrival (ms from the in-stream's start)."""
+        in-stream milliseconds, the in-stream's steady part (from the first chunk's arrival in
+        host memory to its end: every H2D, none of the sender's start-up or first D2H) and each
+        group's arrival (ms from the in-stream's start)."""
         ev = self.last_timing
         if not ev:
             return None
-        return {"out_ms": ev["o0"].elapsed_time(ev["o1"]), "in_ms": ev["i0"].elapsed_time(ev["i1"]),
-                "group_arrival_ms": {g: ev["i0"].elapsed_time(e) for g, e in ev["groups"].items()}}
+        out = {"out_ms": ev["o0"].elapsed_time(ev["o1"]), "in_ms": ev["i0"].elapsed_time(ev["i1"]),
+               "group_arrival_ms": {g: ev["i0"].elapsed_time(e) for g, e in ev["groups"].items()}}
+        if "i_first" in ev:
+            out["in_steady_ms"] = ev["i_first"].elapsed_time(ev["i1"])
+        return out
 
     def wait_streams(self, stream) -> None:
         """Make ``stream`` wait for this round's lane work (both directions)."""

@@ -214,9 +214,10 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
     memory, D2H and H2D pipelined in chunks, ``reps`` timed rounds after ``warmup``: at world 2 the
     exact pattern of the N = 2 halo, and at any world every GPU's PCIe link busy in both
     directions while host memory serves all of them. Per rank: the out rate (its D2H stream's
-    bytes / time) and the in rate (bytes / time from the in stream's start to its last H2D: the
-    pipelined lane end to end), medians over the reps, HIP events on the lane's streams (host
-    clock on CPU tensors). Collective (``agree(ok)``: the control plane's all-ranks AND; a failure
+    bytes / time) and the in rate (bytes / time from the first chunk's arrival in host memory to
+    the last H2D: the pipelined lane's steady rate, free of the ranks' start skew; the planner
+    adds the pipeline's fill separately), medians over the reps, HIP events on the lane's streams
+    (host clock on CPU tensors). Collective (``agree(ok)``: the control plane's all-ranks AND; a failure
     on any rank raises on every rank). Returns {"rates":
     {(a, LANE_OUT): GB/s, (LANE_IN, b): GB/s}, "out_GBps": [per rank], "in_GBps": [per rank],
     "elems": elems, "chunk_elems": c}, identical on every rank (all-reduced)."""
@@ -256,7 +257,7 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
                     torch.cuda.synchronize(dev)
                     tm = lane.timing_ms()
                     outs.append(tm["out_ms"])
-                    ins.append(tm["in_ms"])
+                    ins.append(tm.get("in_steady_ms", tm["in_ms"]))
                 else:
                     dt = (time.perf_counter() - t0) * 1e3
                     outs.append(dt)
