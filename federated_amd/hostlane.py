@@ -87,7 +87,8 @@ class _Segment:
             self.mm = mmap.mmap(fd, self.size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
             os.close(fd)
-        self.base = ctypes.addressof(ctypes.c_char.from_buffer(self.mm))
+        self._anchor = ctypes.c_char.from_buffer(self.mm)  # exports of the mapping: dropped in close()
+        self.base = ctypes.addressof(self._anchor)
         self.words = (ctypes.c_uint32 * (FLAG_BYTES // 4)).from_buffer(self.mm, self.data_bytes)
         self.data = torch.frombuffer(self.mm, dtype=torch.float32, count=2 * self.elems) if self.elems else None
         self.dev_base = None
@@ -111,9 +112,18 @@ class _Segment:
         return int(self.words[i])
 
     def close(self) -> None:
+        """Unpin, drop this object's exports of the mapping and unmap it (the pages go once the
+        peer has unmapped too; the name was unlinked at open)."""
         if self._lib is not None:
             self._lib.cfa_host_unregister(ctypes.c_void_p(self.base))
             self._lib = None
+        if self.mm is not None:
+            self.data = self.words = self._anchor = None
+            try:
+                self.mm.close()
+            except BufferError:  # a caller still holds a view of the segment: it stays mapped
+                pass
+            self.mm = None
 
 
 def _reached(word: int, value: int) -> bool:
