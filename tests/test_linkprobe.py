@@ -109,3 +109,15 @@ def test_round_model_compute_bound_and_contention():
 
 def test_round_model_without_exchange_is_the_mixes():
     assert predict_round_ms([], [], 5, 0.2, 0.5) == pytest.approx(1.0)
+
+
+def test_round_model_waits_for_the_host_lane():
+    """With the host lane a boundary set waits for both paths: here its lane pieces land at 7 ms,
+    after its xGMI group (4 ms), so the set starts at 7 ms; the exchange lasts until the lane's
+    end (8 ms), so mixes started before then are stretched; no lane pieces (None) = xGMI only."""
+    t = predict_round_ms([2.0, 2.0], [(1, 4)], 2, 0.1, 0.0, lane_ready_ms=[7.0], lane_end_ms=8.0)
+    assert t == pytest.approx(max(7.0 + 4 * 0.1, 8.0))
+    t = predict_round_ms([2.0, 2.0], [(1, 4)], 2, 0.1, 0.0, lane_ready_ms=[None], lane_end_ms=0.0)
+    assert t == pytest.approx(4.0 + 4 * 0.1)
+    stretched = predict_round_ms([0.5], [(0, 2)], 20, 0.15, 0.2, lane_ready_ms=[0.2], lane_end_ms=1.0)
+    assert stretched > predict_round_ms([0.5], [(0, 2)], 20, 0.15, 0.2)  # the lane keeps running past 0.5 ms
