@@ -172,7 +172,6 @@ class HostLane:
         self.in_seg: Dict[int, _Segment] = {}
         self._lib = None
         self._status = None
-        self._events: Dict[int, object] = {}
         self.last_timing = None
 
     # -- setup --------------------------------------------------------------------------------
@@ -344,7 +343,6 @@ class HostLane:
             ev["i1"].record(is_)
             ev["groups"] = events
         self.last_timing = ev
-        self._events = events
         return events
 
     def timing_ms(self) -> Optional[dict]:
