@@ -190,3 +190,48 @@ def test_host_lane_rounds_gloo(world, D):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
+
+
+def _absent_peer_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+
+        from federated_amd.halo import Message
+        from federated_amd.hostlane import HostLane, new_token
+        from federated_amd.linkprobe import agree_gloo
+        tok = [new_token() if rank == 0 else None]
+        dist.broadcast_object_list(tok, src=0)
+        bufs = {"send": torch.full((4096,), float(rank)), "recv": torch.zeros(4096)}
+        msgs = [Message(0, a, 1 - a, "send", 0, "recv", 0, 4096, lane=True) for a in range(2)]
+        lane = HostLane.open(rank, [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank],
+                             lambda k: bufs[k], "cpu", tok[0], agree_gloo, chunk_elems=1024, timeout_s=1.0)
+        out = None
+        if rank == 0:  # rank 1 never sends: rank 0's receive times out, loudly and boundedly
+            t0 = time.monotonic()
+            try:
+                lane.run()
+                out = "no error"
+            except RuntimeError as exc:
+                out = ("timeout" if "timed out" in str(exc) else str(exc), time.monotonic() - t0)
+        agree_gloo(True)
+        lane.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_absent_peer_times_out_loudly():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 34100 + (os.getpid() % 997)
+    procs = [ctx.Process(target=_absent_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    kind, seconds = res[0]
+    assert kind == "timeout" and 0.9 < seconds < 10.0
