@@ -1103,10 +1103,10 @@ def main():
         rates = probe["plan_rates"] or (probe["result"] or {}).get("rates")
         if rates:
             from federated_amd.halo import RoutePlan
-            from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS
+            from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS, first_chunk_elems
             msg = probe["message_us"]
-            out["predicted_ms"] = round(plan.predicted_ms(rates, message_us=msg,
-                                                          lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4), 4)
+            out["predicted_ms"] = round(plan.predicted_ms(
+                rates, message_us=msg, lane_chunk_bytes=first_chunk_elems(DEFAULT_CHUNK_ELEMS) * 4), 4)
             out["direct_predicted_ms"] = round(RoutePlan(world, plan.transfers, relay=False).predicted_ms(
                 rates, message_us=msg), 4)
         return out

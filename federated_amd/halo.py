@@ -347,8 +347,9 @@ class RoutePlan:
 
     def predicted_ms(self, rates_gbps: Dict[Tuple[int, int], float], elem_bytes: int = 4,
                      message_us: float = 0.0, lane_chunk_bytes: int = 0) -> float:
-        """Sum of ``predicted_group_ms``; with lane messages, plus the lane pipeline's fill: one
-        ``lane_chunk_bytes`` chunk D2H before the first H2D can start, at the slowest lane rate."""
+        """Sum of ``predicted_group_ms``; with lane messages, plus the lane pipeline's fill: the
+        first chunk (``lane_chunk_bytes``, ``hostlane.first_chunk_elems``) D2H before the first
+        H2D can start, at the slowest lane rate."""
         t = sum(self.predicted_group_ms(rates_gbps, elem_bytes, message_us))
         if lane_chunk_bytes and any(m.lane for g in self.groups for m in g):
             lane_rates = [r for l, r in rates_gbps.items() if is_lane_link(l) and r > 0]

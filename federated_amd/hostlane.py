@@ -42,6 +42,7 @@ from .halo import ALIGN, Message
 FLAG_BYTES = 4096
 READY, ACK = 0, 16            # u32 word indices in a segment's flag page (64 bytes apart)
 DEFAULT_CHUNK_ELEMS = 4 << 20  # 16 MiB fp32: the probe's best D2H + H2D overlap (r05_host_lane_probe)
+RAMP = 3  # a pair's round starts with chunks of 1/8, 1/4, 1/2 of that: the H2D starts after 2 MiB
 DEFAULT_TIMEOUT_S = 60.0
 SHM_DIR = "/dev/shm"
 
@@ -57,14 +58,27 @@ def lane_layout(msgs: Sequence[Message], align: int = ALIGN) -> Tuple[List[int],
     return offs, n
 
 
-def lane_chunks(msgs: Sequence[Message], offs: Sequence[int], chunk_elems: int) -> List[Tuple[int, int, int, int]]:
+def first_chunk_elems(chunk_elems: int, ramp: int = RAMP) -> int:
+    """Elements of a pair's first chunk in a round (what the receiver waits for before its first
+    H2D can start: the lane pipeline's fill)."""
+    return max(ALIGN, (int(chunk_elems) >> ramp) // ALIGN * ALIGN)
+
+
+def lane_chunks(msgs: Sequence[Message], offs: Sequence[int], chunk_elems: int,
+                ramp: int = RAMP) -> List[Tuple[int, int, int, int]]:
     """The pair's copies of one round in order: (message index, element offset within the
-    message, elements, segment offset), messages cut in pieces of at most ``chunk_elems``."""
-    out = []
+    message, elements, segment offset). Messages are cut in pieces of ``chunk_elems``, except the
+    round's first ``ramp`` pieces, which grow from chunk_elems / 2**ramp by doubling (aligned), so
+    the receiver's first H2D waits for a small D2H only."""
+    out, k = [], 0
     for i, m in enumerate(msgs):
-        for lo in range(0, m.count, chunk_elems):
-            n = min(chunk_elems, m.count - lo)
+        lo = 0
+        while lo < m.count:
+            size = chunk_elems if k >= ramp else first_chunk_elems(chunk_elems, ramp - k)
+            n = min(size, m.count - lo)
             out.append((i, lo, n, offs[i] + lo))
+            lo += n
+            k += 1
     return out
 
 

@@ -475,10 +475,10 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
         tr = ring_transfers(gd, L, hl, hr, P, slice_world=gp, slice_bounds=bounds)
         if not staged:
             tr = [type(t)(0, t.src, t.dst, t.src_key, t.dst_key, t.lo, t.hi) for t in tr]
-        from .hostlane import DEFAULT_CHUNK_ELEMS
+        from .hostlane import DEFAULT_CHUNK_ELEMS, first_chunk_elems
         chunk = int(lane_chunk_elems or DEFAULT_CHUNK_ELEMS)
         route, route_choice = choose_route(world, tr, relay=relay, rates_gbps=link_rates, message_us=message_us,
-                                           lane_chunk_bytes=chunk * 4)
+                                           lane_chunk_bytes=first_chunk_elems(chunk) * 4)
         if route.lane and (lane_token is None or lane_agree is None):
             raise ValueError("the chosen route uses the host lane: make_ring_shard needs lane_token and lane_agree")
     Pr = bounds[p + 1] - bounds[p]

@@ -113,10 +113,19 @@ def test_layout_and_chunks():
             Message(1, 0, 1, ("models", 2), 0, ("left", 2), 0, 64, lane=True)]
     offs, n = lane_layout(msgs)
     assert offs == [0, 1024, 1216] and n == 1280
-    ch = lane_chunks(msgs, offs, 512)
+    ch = lane_chunks(msgs, offs, 512, ramp=0)
     assert ch == [(0, 0, 512, 0), (0, 512, 488, 512), (1, 0, 130, 1024), (2, 0, 64, 1216)]
-    for i, m in enumerate(msgs):  # every element of every message exactly once
-        assert sum(c for j, _, c, _ in ch if j == i) == m.count
+    # the default ramp: the round's first pieces 64, 128, 256 elements, then 512
+    ch = lane_chunks(msgs, offs, 512)
+    assert ch == [(0, 0, 64, 0), (0, 64, 128, 64), (0, 192, 256, 192), (0, 448, 512, 448), (0, 960, 40, 960),
+                  (1, 0, 130, 1024), (2, 0, 64, 1216)]
+    for ramp in (0, 3):
+        ch = lane_chunks(msgs, offs, 512, ramp=ramp)
+        for i, m in enumerate(msgs):  # every element of every message exactly once, in order
+            pieces = [(lo, c) for j, lo, c, _ in ch if j == i]
+            assert pieces[0][0] == 0 and sum(c for _, c in pieces) == m.count
+            assert all(a[0] + a[1] == b[0] for a, b in zip(pieces, pieces[1:]))
+            assert all(lo % 64 == 0 for lo, _ in pieces)
 
 
 def test_sequence_order_wraps():

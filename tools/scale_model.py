@@ -44,7 +44,7 @@ def exchange_ms(world, partition, D, h, P, link_gbps, lane_gbps, groups=None):
     """The chosen plan's predicted exchange time at uniform link rates plus (lane_gbps > 0) the
     host lane's, and the MB it puts on the lane."""
     from federated_amd.halo import LANE_IN, LANE_OUT, choose_route
-    from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS
+    from federated_amd.hostlane import DEFAULT_CHUNK_ELEMS, first_chunk_elems
     gd, gp = partition_shape(partition, world, D, groups)
     if gd < 2:
         return 0.0, 0.0
@@ -53,8 +53,9 @@ def exchange_ms(world, partition, D, h, P, link_gbps, lane_gbps, groups=None):
     if lane_gbps > 0:
         rates.update({(a, LANE_OUT): lane_gbps for a in range(world)})
         rates.update({(LANE_IN, a): lane_gbps for a in range(world)})
-    plan, _ = choose_route(world, tr, rates_gbps=rates, lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4)
-    return plan.predicted_ms(rates, lane_chunk_bytes=DEFAULT_CHUNK_ELEMS * 4), plan.lane_elems() * 4 / 1e6
+    fill = first_chunk_elems(DEFAULT_CHUNK_ELEMS) * 4
+    plan, _ = choose_route(world, tr, rates_gbps=rates, lane_chunk_bytes=fill)
+    return plan.predicted_ms(rates, lane_chunk_bytes=fill), plan.lane_elems() * 4 / 1e6
 
 
 def main():
