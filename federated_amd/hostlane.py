@@ -255,7 +255,7 @@ class HostLane:
     def _plan_round(self) -> None:
         """Per pair: the copies of a round in group order (the sender interleaves its peers group
         by group, so every receiver's early stages leave first)."""
-        self._out_plan = []  # (group, dst, seg, chunk number, seg offset, src view slice)
+        self._out_plan = []  # (group, dst, chunk number, segment offset, source slice)
         per_dst = {}
         for dst, ms in self.out_msgs.items():
             offs, n, chunks = self._layout(ms)
