@@ -144,7 +144,12 @@ def from_lines(path):
         route = c.get("halo_route") or {}
         if links.get("median_GBps") and route.get("critical_MB") and dc.get("t_mix_ms") is not None:
             L = c.get("devices_per_gpu") or 0
-            halo = route["critical_MB"] * 1e6 / (links["median_GBps"] * 1e9) * 1e3 + dc.get("tail_ms", 0.0)
+            pred = (route.get("autotune") or {}).get("predicted_ms")
+            if route.get("lane") and pred:  # the kept plan's exchange at the probed link and lane rates
+                halo = pred + dc.get("tail_ms", 0.0)
+                row["host_lane_MB"] = route.get("lane_MB")
+            else:
+                halo = route["critical_MB"] * 1e6 / (links["median_GBps"] * 1e9) * 1e3 + dc.get("tail_ms", 0.0)
             comp = L * dc["t_mix_ms"] * (1 + max(0.0, dc.get("delta") or 0.0))
             row["probe_model_ms"] = round(max(comp, halo), 4)
             row["probe_model_speedup"] = round(T1 / max(comp, halo), 2)
