@@ -302,3 +302,10 @@ def test_bench_parses_the_route_and_decomposition_flags(monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py", "--route-tune", "wallclock", "--no-decomposition"])
     a = bench.parse()
     assert a.route_tune == "wallclock" and a.no_decomposition
+    # the host lane: probed and offered by default, off on request
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    a = bench.parse()
+    assert a.host_lane == "auto" and a.lane_probe_mb == 256.0
+    monkeypatch.setattr("sys.argv", ["bench.py", "--host-lane", "off", "--lane-probe-mb", "64"])
+    a = bench.parse()
+    assert a.host_lane == "off" and a.lane_probe_mb == 64.0
