@@ -180,6 +180,74 @@ def test_bench_plan_world8_issue_sequence_and_replay(stub):
                 assert torch.equal(src, full[j]), (shard.plan.rank, g, j)
 
 
+class RecordingLane:
+    """Stands in for hostlane.HostLane in a one-process run of all ranks: records that the round
+    issued its lane part (the lane's own protocol is tested in test_host_lane.py)."""
+
+    def __init__(self):
+        self.rounds = 0
+
+    def run(self, stream=None, timing=False):
+        self.rounds += 1
+        return {}
+
+
+def test_bench_plan_world8_with_the_host_lane(stub):
+    """The bench's N = 8 plan with the host lane offered (every link alike: the planner keeps relays
+    AND the lane): RCCL is handed exactly the plan's transport messages (no lane piece reaches it),
+    they pair across ranks, and replaying them as copies plus the lane pieces as copies delivers
+    every halo row."""
+    from federated_amd.halo import RoutePlan, ring_transfers
+    from federated_amd.population import RingPopulationShard, RingShardPlan
+    world, D, h, P = 8, 128, 4, 65_537
+    L = D // world
+    plan = RoutePlan(world, ring_transfers(world, L, h, h, P), relay=True, lane=True)
+    assert plan.relay and plan.lane and plan.lane_elems() > 0
+    full = [torch.randn(P, generator=torch.Generator().manual_seed(900 + g)) for g in range(D)]
+    shards, comms, lanes = [], [], []
+    for r in range(world):
+        rc = stub_transport(stub, r, world)
+        shard = RingPopulationShard(RingShardPlan(r, world, L, h), P, "cpu", ViaRccl(rc), None, route=plan, rank=r)
+        shard.lane = RecordingLane()
+        for i in range(L):
+            shard.models[i] = full[shard.plan.first + i]
+        shard.exchange(FakeStream(0x6000 + r))
+        shards.append(shard)
+        comms.append(rc.comm)
+        lanes.append(shard.lane)
+    assert all(ln.rounds == 1 for ln in lanes)
+    logs = [parse(read_log(stub, c)) for c in comms]
+    n_lane = 0
+    for r, shard in enumerate(shards):
+        routed = shard.routed()
+        sent = [(op, peer, cnt) for grp in logs[r] for op, peer, cnt, _, _ in grp]
+        expect = []
+        for g in range(len(plan.groups)):
+            sends, recvs = plan.rank_ops(r, g)
+            expect += [("send", m.dst, m.count) for m in sends] + [("recv", m.src, m.count) for m in recvs]
+        assert sent == expect, f"rank {r}"
+        n_lane += len(plan.lane_ops(r)[0])
+    assert n_lane > 0
+    # replay: the RCCL groups in order, then the lane pieces (they land by the last group here)
+    for g in range(len(plan.groups)):
+        for a in range(world):
+            for b in range(world):
+                sends = [(c, p) for op, peer, c, p, _ in logs[a][g] if op == "send" and peer == b]
+                recvs = [(c, p) for op, peer, c, p, _ in logs[b][g] if op == "recv" and peer == a]
+                assert [c for c, _ in sends] == [c for c, _ in recvs], (g, a, b)
+                for (c, src), (_, dst) in zip(sends, recvs):
+                    ctypes.memmove(dst, src, c * 4)
+    for a in range(world):
+        for m in plan.lane_ops(a)[0]:
+            src = shards[a].buffer(m.src_key).reshape(-1)[m.src_off:m.src_off + m.count]
+            shards[m.dst].buffer(m.dst_key).reshape(-1)[m.dst_off:m.dst_off + m.count].copy_(src)
+    for shard in shards:
+        for i in shard.plan.boundary():
+            g = shard.plan.first + i
+            for src, j in zip(shard.sources(i), shard.plan.neighbours(g)):
+                assert torch.equal(src, full[j]), (shard.plan.rank, g, j)
+
+
 def routed_view(routed, shard, key, off, cnt):
     buf = routed.relay[key[1]] if isinstance(key, tuple) and key[0] == "relay" else shard.buffer(key)
     return buf.reshape(-1)[off:off + cnt].data_ptr()
