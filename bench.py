@@ -1041,8 +1041,9 @@ def main():
         lane["token"] = tok[0]
         t_lane = time.perf_counter()
         try:
+            # a lane whose words never arrive on this node costs one 15 s timeout, then is left out
             lane["result"] = probe_lane(rank, world, torch.device("cuda", device), tok[0] + "p", agree_all,
-                                        elems=int(args.lane_probe_mb * 1e6 / 4))
+                                        elems=int(args.lane_probe_mb * 1e6 / 4), timeout_s=15.0)
         except Exception as exc:
             lane["error"] = f"{type(exc).__name__}: {exc}"
             print(f"[bench rank {rank}] host lane probe failed: {lane['error']}", file=sys.stderr, flush=True)
