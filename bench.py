@@ -1182,6 +1182,25 @@ def main():
             headline, headline_exchanges = "params", False
             res = measure_headline("params")
         shard, info, autotune, elapsed, durations, launches_per_step = res
+    # N > 1: the halo the timed rounds delivered, row by row against the rows their owners hold
+    # (exact 32-bit-pattern checksums), so the line proves the exchange moved the right bytes over
+    # RCCL, the relays and the host lane on this node
+    halo_check = None
+    if world > 1 and info.get("route") is not None:
+        watchdog.enter("halo check")
+
+        def gather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        n_rows, n_bad = shard.halo_check(gather, info["slice"][0])
+        tot = torch.tensor([n_rows, n_bad], dtype=torch.int64)
+        dist.all_reduce(tot)
+        halo_check = {"rows": int(tot[0]), "mismatches": int(tot[1]),
+                      "method": "sum of 32-bit patterns per row, receiver against owner, after the timed rounds"}
+        if halo_check["mismatches"]:
+            print(f"[bench rank {rank}] HALO CHECK FAILED: {n_bad} of {n_rows} halo rows differ from their owners'",
+                  file=sys.stderr, flush=True)
     bytes_total = D * (K + 2) * P * 4 * args.steps  # every device's mix, all ranks (slices sum to P)
     value = bytes_total / elapsed / 1e9
     interior = shard.interior_order()
@@ -1246,6 +1265,7 @@ def main():
                                   "achieved_critical_ms": (decomp or {}).get("exchange_groups_ms_sum")})
                 if route else None,
                 "links": probe["summary"] if probe["error"] is None else {"error": probe["error"]},
+                "halo_check": halo_check,
                 "host_lane": lane_summary() if headline_exchanges else None,
                 "placement": info.get("placement"),
                 "halo_carved": info.get("halo_carved"),
@@ -1529,7 +1549,8 @@ def main():
         dist.all_gather_object(tails, rccl_log_tail(rccl_log, 600))
         if rank == 0:
             result["config"]["rccl_log"] = {str(r): t for r, t in enumerate(tails) if t} or None
-    code = EXIT_TRANSPORT if headline_fallback else (EXIT_LEG if leg_failed else 0)
+    halo_bad = bool(halo_check and halo_check["mismatches"])
+    code = EXIT_TRANSPORT if headline_fallback else (EXIT_LEG if (leg_failed or halo_bad) else 0)
     if rank == 0:
         result["config"]["budget"].update({"skipped": skipped, "left_s": round(budget.left(), 1)})
         result["exit_status"] = code

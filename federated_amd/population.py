@@ -96,6 +96,12 @@ class RingShardPlan:
         return sends, recvs
 
 
+def row_checksum(t: torch.Tensor) -> int:
+    """Exact, order-independent checksum of an fp32 row: the sum of its 32-bit patterns in int64
+    (any single changed element changes it; computed where the row lives)."""
+    return int(t.contiguous().view(torch.int32).to(torch.int64).sum().item())
+
+
 def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
     """Do the byte ranges of two tensors intersect (same device)?"""
     if a.device != b.device or a.numel() == 0 or b.numel() == 0:
@@ -332,6 +338,25 @@ class RingPopulationShard:
             self.mix_device(i, stream)
             if timer:
                 timer(i, False)
+
+    def halo_check(self, gather, slice_lo: int = 0) -> Tuple[int, int]:
+        """After an exchange: every halo row against the row its owner holds, by ``row_checksum``.
+        ``gather(obj)`` returns every rank's ``obj`` (torch.distributed.all_gather_object); each
+        rank contributes the rows other shards read (its first ``hr`` and last ``hl``), keyed by
+        (global device, ``slice_lo``) so the slices of a hybrid partition stay apart. Collective.
+        Returns (halo rows checked, rows that differ) on this rank."""
+        p = self.plan
+        own = {(p.first + i, int(slice_lo)): row_checksum(self.models[i])
+               for i in range(p.L) if p.world > 1 and (i < p.hr or i >= p.L - p.hl)}
+        table = {}
+        for part in gather(own):
+            table.update(part or {})
+        if p.world == 1:
+            return 0, 0
+        rows = [((p.first - p.hl + q) % p.D, self.halo["left"][q]) for q in range(p.hl)]
+        rows += [((p.first + p.L + q) % p.D, self.halo["right"][q]) for q in range(p.hr)]
+        bad = sum(row_checksum(r) != table.get((g, int(slice_lo))) for g, r in rows)
+        return len(rows), int(bad)
 
     @property
     def route_plan(self):

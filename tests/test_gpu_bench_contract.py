@@ -41,7 +41,8 @@ def test_bench_line_contract():
 N_GT_1_FIELDS = [("value", float), ("ms_per_step", float), ("n_gpus", int), ("exit_status", int),
                  ("config", dict), ("roofline", dict), ("partitions", dict)]
 CONFIG_FIELDS = ["partition", "transport", "comparable", "rccl_version", "halo_route", "cache_reuse", "rows_note",
-                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback", "links", "rccl_log", "host_lane"]
+                 "gpus_visible", "ranks_share_gpus", "budget", "headline_fallback", "links", "rccl_log", "host_lane",
+                 "halo_check"]
 
 
 def _self_launched(extra, timeout=240):
@@ -79,6 +80,8 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     assert at["mode"] == "links" and at["predicted_ms"] > 0
     assert at["plan"].split("+")[0] in ("uniform", "measured", "direct")
     assert at["candidates_predicted_ms"]["uniform"] > 0 and c["halo_route"]["link_cost"] in ("uniform", "measured")
+    # every halo row the timed rounds delivered equals its owner's row (2 ranks x 8 rows)
+    assert c["halo_check"]["rows"] == 16 and c["halo_check"]["mismatches"] == 0
     # the host lane: probed with both ranks on it at once, offered to the plan, reported when used
     hl = c["host_lane"]
     assert len(hl["out_GBps"]) == 2 and min(hl["out_GBps"] + hl["in_GBps"]) > 0

@@ -252,6 +252,13 @@ def _worker(rank, world, port, D, h, P, partition, gd, relay, staged, q, hr=None
         dist.all_gather_object(digests, info.get("route_digest"))
         ok = len(set(digests)) == 1
         shard.exchange()
+
+        def gather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        n, bad = shard.halo_check(gather, lo)  # every halo row equals its owner's (exact checksums)
+        ok &= bad == 0 and n == ((plan.hl + plan.hr) if plan.world > 1 else 0)
         full = [_seeded(g, P).numpy() for g in range(D)]
         alphas = shard.alphas
         for i in range(plan.L):

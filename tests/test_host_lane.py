@@ -175,6 +175,15 @@ def _worker(rank, world, port, D, P, rounds, q):
                 ok &= all(np.array_equal(s, full[j]) for s, j in zip(srcs, nb))
                 got = sequential_mix(shard.models[i].numpy(), srcs, alphas)
                 ok &= np.array_equal(got, sequential_mix(full[g], [full[j] for j in nb], alphas))
+        def gather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        n, bad = shard.halo_check(gather, info["slice"][0])
+        ok &= n == 8 and bad == 0
+        shard.halo["left"][0][7] += 1.0  # one changed element is caught
+        n, bad = shard.halo_check(gather, info["slice"][0])
+        ok &= bad == 1
         lane_in = info["lane"]["in_MB"]
         shard.lane.close()
         q.put((rank, bool(ok), lane_in))
