@@ -41,8 +41,10 @@ from .halo import ALIGN, Message
 
 FLAG_BYTES = 4096
 READY, ACK = 0, 16            # u32 word indices in a segment's flag page (64 bytes apart)
-DEFAULT_CHUNK_ELEMS = 4 << 20  # 16 MiB fp32: the probe's best D2H + H2D overlap (r05_host_lane_probe)
-RAMP = 3  # a pair's round starts with chunks of 1/8, 1/4, 1/2 of that: the H2D starts after 2 MiB
+# 32 MiB fp32 copies: with D2H and H2D at once, 49.6 + 54.7 GB/s against 47.1 + 53.5 at 16 MiB and
+# 39.1 + 40.6 at 2 MiB; 64 MiB adds < 1%, 100 MiB halves the H2D (r05_host_lane_chunk_sweep.jsonl)
+DEFAULT_CHUNK_ELEMS = 8 << 20
+RAMP = 3  # a pair's round starts with chunks of 1/8, 1/4, 1/2 of that: the H2D starts after 4 MiB
 DEFAULT_TIMEOUT_S = 60.0
 SHM_DIR = "/dev/shm"
 

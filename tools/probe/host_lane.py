@@ -80,7 +80,8 @@ def rates(a):
         return {k: round(v, 2) for k, v in best.items()}
 
     out = {"mode": "rates", "bytes_per_direction": nbytes}
-    for chunk in (100 << 20, 16 << 20):
+    chunks = [int(c) << 20 for c in a.sweep_mb.split(",")] if a.sweep_mb else [100 << 20, 16 << 20]
+    for chunk in chunks:
         tag = f"{chunk >> 20}MB"
         out[f"d2h_alone_{tag}"] = timed([("d2h", lambda s: d2h(s, chunk), s1)])["d2h"]
         out[f"h2d_alone_{tag}"] = timed([("h2d", lambda s: h2d(s, chunk), s2)])["h2d"]
@@ -282,6 +283,7 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=16)
     ap.add_argument("--timeout-s", type=float, default=5.0)
     ap.add_argument("--wall-s", type=float, default=150.0)
+    ap.add_argument("--sweep-mb", default="", help="rates mode: copy sizes in MB (default 100,16)")
     ap.add_argument("--seg", nargs=2)
     ap.add_argument("--child-index", type=int, default=0)
     a = ap.parse_args()
