@@ -275,9 +275,49 @@ def xproc(a):
     return 0 if all(r["rc"] == 0 for r in info.get("children", [])) else 1
 
 
+def probe_child(rank, world, port, sizes_mb, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from federated_amd.hostlane import new_token
+        from federated_amd.linkprobe import agree_gloo, probe_lane
+        out = {}
+        for mb in sizes_mb:
+            tok = [new_token() if rank == 0 else None]
+            dist.broadcast_object_list(tok, src=0)
+            r = probe_lane(rank, world, torch.device("cuda", 0), tok[0], agree_gloo, elems=int(mb * 1e6 / 4),
+                           reps=5, timeout_s=15.0)
+            out[mb] = {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"]}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def probe_sizes(a):
+    """``linkprobe.probe_lane`` itself (two processes on the GPU, as the N = 2 bench runs it) at
+    several message sizes: how far the probed rate depends on the probe's own size."""
+    import multiprocessing as mp
+    sizes = [float(x) for x in a.sweep_mb.split(",")] if a.sweep_mb else [64.0, 256.0, 1024.0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35500 + os.getpid() % 997
+    procs = [ctx.Process(target=probe_child, args=(r, 2, port, sizes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=a.wall_s) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    print(json.dumps({"mode": "probe", "by_size_MB": res[0]}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["rates", "xproc", "child"], default="rates")
+    ap.add_argument("--mode", choices=["rates", "xproc", "child", "probe"], default="rates")
     ap.add_argument("--rows", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--chunk-mb", type=int, default=16)
@@ -291,6 +331,8 @@ def main():
         return rates(a) or 0
     if a.mode == "child":
         return child(a)
+    if a.mode == "probe":
+        return probe_sizes(a)
     return xproc(a)
 
 
