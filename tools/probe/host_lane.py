@@ -6,7 +6,7 @@ interior mixing time; the only other path between two GPUs of a node is each GPU
 host memory (Gen5 x16, 63 GB/s per direction spec). This probe measures what that path gives.
 
 ``--mode rates`` (one process): D2H and H2D copy rates between HBM and pinned host memory, each
-alone and both at once, at two copy sizes; then the headline mix (K = 8 x 25M) alone and while
+alone and both at once, at two copy sizes (or those of ``--sweep-mb``); then the headline mix (K = 8 x 25M) alone and while
 both copy directions run, which gives the copies' cost to the mixes (delta) and the copy rates
 under mixing load.
 
@@ -19,7 +19,11 @@ for back-pressure. Every round the consumer checks the landed rows bit for bit a
 producer's pattern. On a one-GPU box both directions share the one PCIe link, so the rates are
 a lower bound for two GPUs.
 
-Usage (GPU box): python tools/probe/host_lane.py --mode rates | --mode xproc [--rounds 12]"""
+``--mode probe``: ``linkprobe.probe_lane`` itself, two processes on the GPU, at the message sizes
+of ``--sweep-mb`` (default 64, 256, 1024 MB per rank).
+
+Usage (GPU box): python tools/probe/host_lane.py --mode rates [--sweep-mb 2,4,...] | --mode xproc
+[--rounds 12] | --mode probe"""
 import argparse
 import ctypes
 import json
