@@ -99,7 +99,9 @@ class _Segment:
         fd = os.open(path, flags, 0o600)
         try:
             if create:
-                os.ftruncate(fd, self.size)
+                # reserve the pages now: a full /dev/shm fails here (ENOSPC, reported through the
+                # open's agreement) instead of a SIGBUS at the first copy into a sparse file
+                os.posix_fallocate(fd, 0, self.size)
             self.mm = mmap.mmap(fd, self.size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
             os.close(fd)
