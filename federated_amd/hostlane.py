@@ -4,8 +4,8 @@ Two GPUs of an MI355X node share exactly one xGMI link, so with the population s
 blocks over N = 2 GPUs the whole ring halo (800 MB per rank per round at the bench's shape) rides
 one link direction, and at N = 4 two; the mixes of a round take half that long.
 The only other path between two GPUs is each GPU's PCIe Gen5 x16 link to host memory (63 GB/s
-per direction spec; 55 GB/s D2H and H2D measured, 47 + 53 GB/s with both at once,
-``profiles/r05_host_lane_probe.jsonl``). The reference has no such path to mirror: its devices
+per direction spec; 55 GB/s D2H and H2D measured, 50 + 55 GB/s with both at once in 32 MB
+copies, ``profiles/r05_host_lane_chunk_sweep.jsonl``). The reference has no such path to mirror: its devices
 exchange models as files (TF1 ``cfa.py:119-130``).
 
 A lane piece (``halo.RoutePlan`` with ``lane=True``) goes:
