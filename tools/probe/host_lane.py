@@ -290,12 +290,12 @@ def probe_child(rank, world, port, sizes_mb, q):
         from federated_amd.hostlane import new_token
         from federated_amd.linkprobe import agree_gloo, probe_lane
         out = {}
-        for mb in sizes_mb:
+        for i, mb in enumerate(sizes_mb):
             tok = [new_token() if rank == 0 else None]
             dist.broadcast_object_list(tok, src=0)
             r = probe_lane(rank, world, torch.device("cuda", 0), tok[0], agree_gloo, elems=int(mb * 1e6 / 4),
                            reps=5, timeout_s=15.0)
-            out[mb] = {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"]}
+            out[f"{i}:{mb:g}"] = {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"]}  # in call order
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
