@@ -249,8 +249,10 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
     except Exception as exc:
         err = f"{type(exc).__name__}: {exc}"
     if agree(err is None):
-        try:
-            for _ in range(reps):
+        # one agreement per rep, on every rank alike (the same number of collectives whatever
+        # fails): each rep starts with every rank drained, so no ack wait or start skew is timed
+        for _ in range(reps):
+            try:
                 t0 = time.perf_counter()
                 lane.run(stream, timing=gpu)
                 if gpu:
@@ -263,12 +265,16 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
                     outs.append(dt)
                     ins.append(dt)
                 lane.check()
+            except Exception as exc:
+                err = f"{type(exc).__name__}: {exc}"
+            if not agree(err is None):
+                err = err or "a lane probe rep failed on another rank"
+                break
+        if err is None:
             src = (rank - 1) % world
             got = (float(bufs["recv"][0].item()), float(bufs["recv"][-1].item()))
             if got != (float(src), float(src)):
-                raise RuntimeError(f"lane probe: rank {rank} received {got}, not rank {src}'s rows")
-        except Exception as exc:
-            err = f"{type(exc).__name__}: {exc}"
+                err = f"lane probe: rank {rank} received {got}, not rank {src}'s rows"
     else:
         err = err or "the warm-up failed on another rank"
     lane.close()
