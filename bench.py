@@ -1050,6 +1050,9 @@ def main():
         if lane["result"] is not None:
             lane["result"]["wall_s"] = round(time.perf_counter() - t_lane, 2)
             probe["plan_rates"] = {**probe["plan_rates"], **lane["result"]["rates"]}
+        topo = [None] * world
+        dist.all_gather_object(topo, gpu_topology(device))
+        lane["topology"] = topo
 
     def lane_summary():
         if args.host_lane == "off":
@@ -1060,7 +1063,8 @@ def main():
         if r is None:
             return None
         return {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"], "message_MB": round(r["elems"] * 4 / 1e6, 1),
-                "chunk_MB": round(r["chunk_elems"] * 4 / 2**20, 2), "timing": r["timing"], "wall_s": r.get("wall_s")}
+                "chunk_MB": round(r["chunk_elems"] * 4 / 2**20, 2), "timing": r["timing"], "wall_s": r.get("wall_s"),
+                "topology": lane.get("topology")}
 
     def build(partition, devices=None, relay=None):
         transport = tstate["transport"]
@@ -1585,6 +1589,27 @@ def rccl_version():
     except Exception:
         return None
     return int(v.value)
+
+
+def gpu_topology(device: int) -> dict:
+    """Where this rank's GPU sits: its PCI address, the NUMA node the kernel reports for it and the
+    CPUs this process may run on (the host lane's D2H / H2D cross that path; read-only sysfs)."""
+    import torch
+    out = {"device": device}
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        out["pci"] = bdf
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as fh:
+            out["numa_node"] = int(fh.read().strip())
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        pass
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        out["cpus"] = f"{cpus[0]}-{cpus[-1]} ({len(cpus)})" if cpus else None
+    except (AttributeError, OSError):
+        pass
+    return out
 
 
 def shard_P(info, P):

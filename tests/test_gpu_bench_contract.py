@@ -85,6 +85,7 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     # the host lane: probed with both ranks on it at once, offered to the plan, reported when used
     hl = c["host_lane"]
     assert len(hl["out_GBps"]) == 2 and min(hl["out_GBps"] + hl["in_GBps"]) > 0
+    assert len(hl["topology"]) == 2 and all("pci" in t for t in hl["topology"])
     assert "uniform+lane" in at["candidates_predicted_ms"]
     if at["plan"].endswith("+lane"):
         assert c["halo_route"]["lane"] and c["halo_route"]["lane_MB"] > 0 and at["host_lane"]["in_MB"] > 0
