@@ -137,7 +137,7 @@ def _seeded(g, P):
     return torch.randn(P, generator=torch.Generator().manual_seed(9100 + g))
 
 
-def _worker(rank, world, port, D, P, rounds, q):
+def _worker(rank, world, port, D, P, rounds, q, partition="devices", gd=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -155,19 +155,22 @@ def _worker(rank, world, port, D, P, rounds, q):
         ok &= all(r > 0 for r in probe["rates"].values())
         rates = _rates(world, 50.0, 50.0)
         shard, info = make_ring_shard(rank, world, D, 4, 4, P, "cpu", TorchTransport(), None, relay=True,
+                                      partition=partition, dev_groups=gd,
                                       link_rates=rates, lane_token=tok[0], lane_agree=agree_gloo,
                                       lane_chunk_elems=256)
         ok &= bool(info["route"]["lane"]) and "+lane" in info["route_choice"]["chosen"]
-        ok &= bool(info["route"]["relay"]) == (world == 8)  # at 8 ranks relays and the lane together
+        if partition == "devices":
+            ok &= bool(info["route"]["relay"]) == (world == 8)  # at 8 ranks relays and the lane together
+        lo, hi = info["slice"]
         agree_gloo(True)  # every rank has unlinked the names it created
         ok &= not [f for f in os.listdir("/dev/shm") if tok[0] in f]
         plan = shard.plan
         alphas = shard.alphas
         for r in range(rounds):
             for i in range(plan.L):
-                shard.models[i] = _seeded(plan.first + i, P) + r
+                shard.models[i] = (_seeded(plan.first + i, P) + r)[lo:hi]
             shard.exchange()
-            full = [(_seeded(g, P) + r).numpy() for g in range(D)]
+            full = [(_seeded(g, P) + r).numpy()[lo:hi] for g in range(D)]
             for i in range(plan.L):
                 g = plan.first + i
                 nb = plan.neighbours(g)
@@ -191,13 +194,14 @@ def _worker(rank, world, port, D, P, rounds, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,D", [(2, 16), (4, 16), (8, 64)])
-def test_host_lane_rounds_gloo(world, D):
+@pytest.mark.parametrize("world,D,partition,gd", [(2, 16, "devices", None), (4, 16, "devices", None),
+                                                 (8, 64, "devices", None), (4, 16, "hybrid", 2)])
+def test_host_lane_rounds_gloo(world, D, partition, gd):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     P = 5000 + 17
-    port = 33500 + (os.getpid() % 997) + world * 7
-    procs = [ctx.Process(target=_worker, args=(r, world, port, D, P, 4, q)) for r in range(world)]
+    port = 33500 + (os.getpid() % 997) + world * 7 + (gd or 0) * 3
+    procs = [ctx.Process(target=_worker, args=(r, world, port, D, P, 4, q, partition, gd)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
