@@ -321,7 +321,23 @@ def child_env(base: dict, t0: float, status_file: str) -> dict:
     env[STATUS_FILE_ENV] = status_file
     env["PYTHONUNBUFFERED"] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool: dmabuf IPC only
+    set_hw_queues(env)  # the ranks are N > 1 processes
     return env
+
+
+HW_QUEUES = "8"
+
+
+def set_hw_queues(environ=None) -> str:
+    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES = 8 unless the caller set it. HIP maps
+    a process's streams onto that many hardware queues (4 by default) and streams beyond share one,
+    running in order: a kernel that waits for a peer (RCCL's, the host lane's wait kernel) then
+    holds back every stream on its queue, the compute stream included (`tools/probe/hw_queues.py`:
+    with 4 queues one of 7 streams stalled behind a parked wait, with 8 queues none of 9). A round
+    at N > 1 runs the compute, comm and two lane streams besides torch's own."""
+    env = os.environ if environ is None else environ
+    env.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
+    return env["GPU_MAX_HW_QUEUES"]
 
 
 def setup_rccl_diagnostics(rank: int, environ=None):
@@ -934,6 +950,8 @@ def main():
         wd = args.total_seconds + 90.0 if args.total_seconds > 0 else 900.0
     watchdog = Watchdog(wd, rank, t0)
     rccl_log = setup_rccl_diagnostics(rank) if world > 1 else None  # before anything opens RCCL
+    if world > 1:
+        set_hw_queues()  # before torch loads the HIP runtime
     route_tune = "none" if args.no_autotune else args.route_tune
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
@@ -1277,6 +1295,7 @@ def main():
                 "gpus_visible": ndev,
                 "ranks_share_gpus": world > ndev,
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
                 "rows_note": (f"each rank's rows are {shard_P(info, P)} elements, so a mix's {K + 1}-row window "

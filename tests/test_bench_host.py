@@ -132,6 +132,11 @@ def test_child_env_sets_origin_and_status_and_drops_rank_vars():
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["OMP_NUM_THREADS"] == "16"
     assert env["PYTHONUNBUFFERED"] == "1"
     assert bench.child_env({}, 0.0, "x")["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # N > 1 ranks get 8 hardware queues (streams blocked behind a peer wait otherwise) unless set
+    assert env["GPU_MAX_HW_QUEUES"] == "8"
+    assert bench.child_env({"GPU_MAX_HW_QUEUES": "16"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "16"
+    e = {}
+    assert bench.set_hw_queues(e) == "8" and e == {"GPU_MAX_HW_QUEUES": "8"}
 
 
 FAKE_TORCHRUN = r'''#!/usr/bin/env python3

@@ -100,8 +100,9 @@ def _worker(rank, world, port, D, P, rounds, q):
         dist.destroy_process_group()
 
 
-def test_host_lane_two_processes_match_the_oracle(gpu):
+def test_host_lane_two_processes_match_the_oracle(gpu, monkeypatch):
     import torch.multiprocessing as mp
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")  # as bench.py's ranks (bench.set_hw_queues)
     from federated_amd.population import RingShardPlan
     from oracle.cfa_oracle import sequential_mix
     D, P, rounds, world = 16, 300_037, 3, 2
