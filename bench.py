@@ -329,14 +329,20 @@ HW_QUEUES = "8"
 
 
 def set_hw_queues(environ=None) -> str:
-    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES = 8 unless the caller set it. HIP maps
+    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES raised to at least 8 (a larger value
+    is kept; the pool's boxes export HIP's default of 4 explicitly). HIP maps
     a process's streams onto that many hardware queues (4 by default) and streams beyond share one,
     running in order: a kernel that waits for a peer (RCCL's, the host lane's wait kernel) then
     holds back every stream on its queue, the compute stream included (`tools/probe/hw_queues.py`:
     with 4 queues one of 7 streams stalled behind a parked wait, with 8 queues none of 9). A round
     at N > 1 runs the compute, comm and two lane streams besides torch's own."""
     env = os.environ if environ is None else environ
-    env.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
+    try:
+        cur = int(env.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        cur = 0
+    if cur < int(HW_QUEUES):
+        env["GPU_MAX_HW_QUEUES"] = HW_QUEUES
     return env["GPU_MAX_HW_QUEUES"]
 
 

@@ -135,6 +135,7 @@ def test_child_env_sets_origin_and_status_and_drops_rank_vars():
     # N > 1 ranks get 8 hardware queues (streams blocked behind a peer wait otherwise) unless set
     assert env["GPU_MAX_HW_QUEUES"] == "8"
     assert bench.child_env({"GPU_MAX_HW_QUEUES": "16"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "16"
+    assert bench.child_env({"GPU_MAX_HW_QUEUES": "4"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "8"  # raised
     e = {}
     assert bench.set_hw_queues(e) == "8" and e == {"GPU_MAX_HW_QUEUES": "8"}
 
