@@ -313,7 +313,7 @@ def child_command(argv, n: int, port: int, python: str = None) -> list:
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
-def child_env(base: dict, t0: float, status_file: str) -> dict:
+def child_env(base: dict, t0: float, status_file: str, ranks: int = 0) -> dict:
     env = dict(base)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -321,28 +321,53 @@ def child_env(base: dict, t0: float, status_file: str) -> dict:
     env[STATUS_FILE_ENV] = status_file
     env["PYTHONUNBUFFERED"] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool: dmabuf IPC only
-    set_hw_queues(env)  # the ranks are N > 1 processes
+    set_hw_queues(env, ranks)  # the ranks are N > 1 processes
     return env
 
 
-HW_QUEUES = "8"
+HW_QUEUES = "8"           # ranks sharing a GPU (one-GPU rehearsals)
+HW_QUEUES_OWN_GPU = "16"  # one rank per GPU
 
 
-def set_hw_queues(environ=None) -> str:
-    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES raised to at least 8 (a larger value
-    is kept; the pool's boxes export HIP's default of 4 explicitly). HIP maps
+def visible_gpu_count(environ=None) -> int:
+    """GPUs this process could see, without loading HIP: the *_VISIBLE_DEVICES list when set, else
+    the KFD topology's GPU nodes (0 when neither can be read)."""
+    env = os.environ if environ is None else environ
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(k)
+        if v is not None and v.strip():
+            return len([x for x in v.split(",") if x.strip()])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for d in os.listdir(base):
+            try:
+                with open(os.path.join(base, d, "gpu_id")) as fh:
+                    n += int(fh.read().strip() or "0") != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    return n
+
+
+def set_hw_queues(environ=None, ranks_here: int = 0) -> str:
+    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES raised to at least 16 when each of the
+    node's ``ranks_here`` ranks has a GPU of its own, else 8 (a larger value is kept; the pool's
+    boxes export HIP's default of 4 explicitly). HIP maps
     a process's streams onto that many hardware queues (4 by default) and streams beyond share one,
     running in order: a kernel that waits for a peer (RCCL's, the host lane's wait kernel) then
     holds back every stream on its queue, the compute stream included (`tools/probe/hw_queues.py`:
     with 4 queues one of 7 streams stalled behind a parked wait, with 8 queues none of 9). A round
     at N > 1 runs the compute, comm and two lane streams besides torch's own."""
     env = os.environ if environ is None else environ
+    want = HW_QUEUES_OWN_GPU if 0 < ranks_here <= visible_gpu_count(env) else HW_QUEUES
     try:
         cur = int(env.get("GPU_MAX_HW_QUEUES", "0"))
     except ValueError:
         cur = 0
-    if cur < int(HW_QUEUES):
-        env["GPU_MAX_HW_QUEUES"] = HW_QUEUES
+    if cur < int(want):
+        env["GPU_MAX_HW_QUEUES"] = want
     return env["GPU_MAX_HW_QUEUES"]
 
 
@@ -395,7 +420,7 @@ def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python
     print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
     # the launcher stays in this process's group, so an outer time limit that signals the group
     # (coreutils timeout does) reaches every rank too
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file),
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file, n),
                             text=True, bufsize=1)
     killed = threading.Event()
 
@@ -695,6 +720,19 @@ def seed_shard(shard, info, P):
     del full
 
 
+_COMM_STREAMS = {}
+
+
+def comm_stream():
+    """One exchange stream per device for the whole run (headline, decomposition, legs): every new
+    stream may take a hardware queue another active stream holds (``set_hw_queues``)."""
+    import torch
+    dev = torch.cuda.current_device()
+    if dev not in _COMM_STREAMS:
+        _COMM_STREAMS[dev] = torch.cuda.Stream()
+    return _COMM_STREAMS[dev]
+
+
 def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
     """Warmup, then EXACTLY ``steps`` rounds bracketed by barrier + synchronize; returns
     (max-over-ranks seconds, per-launch kernel durations in ms)."""
@@ -702,7 +740,7 @@ def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
     import torch.distributed as dist
 
     compute = torch.cuda.current_stream()
-    comm = torch.cuda.Stream() if shard.plan.world > 1 else None
+    comm = comm_stream() if shard.plan.world > 1 else None
     interior = shard.interior_order()
     if not interior:
         timed_kernel = False
@@ -795,7 +833,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     routed = shard.routed()
     G = len(plan.groups)
     compute = torch.cuda.current_stream()
-    comm = torch.cuda.Stream()
+    comm = comm_stream()
 
     def barrier():
         torch.cuda.synchronize()
@@ -956,8 +994,8 @@ def main():
         wd = args.total_seconds + 90.0 if args.total_seconds > 0 else 900.0
     watchdog = Watchdog(wd, rank, t0)
     rccl_log = setup_rccl_diagnostics(rank) if world > 1 else None  # before anything opens RCCL
-    if world > 1:
-        set_hw_queues()  # before torch loads the HIP runtime
+    if world > 1:  # before torch loads the HIP runtime
+        set_hw_queues(ranks_here=int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     route_tune = "none" if args.no_autotune else args.route_tune
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)

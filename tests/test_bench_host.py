@@ -138,6 +138,13 @@ def test_child_env_sets_origin_and_status_and_drops_rank_vars():
     assert bench.child_env({"GPU_MAX_HW_QUEUES": "4"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "8"  # raised
     e = {}
     assert bench.set_hw_queues(e) == "8" and e == {"GPU_MAX_HW_QUEUES": "8"}
+    # one rank per GPU: 16 queues; ranks sharing a GPU (a one-GPU rehearsal): 8
+    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}) == 8
+    e = {"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7", "GPU_MAX_HW_QUEUES": "4"}
+    assert bench.set_hw_queues(e, ranks_here=8) == "16"
+    e = {"HIP_VISIBLE_DEVICES": "0", "GPU_MAX_HW_QUEUES": "4"}
+    assert bench.set_hw_queues(e, ranks_here=2) == "8"
+    assert bench.child_env({"HIP_VISIBLE_DEVICES": "0,1"}, 0.0, "x", ranks=2)["GPU_MAX_HW_QUEUES"] == "16"
 
 
 FAKE_TORCHRUN = r'''#!/usr/bin/env python3
