@@ -80,6 +80,8 @@ def test_self_launched_n2_line_matches_the_documented_schema():
     assert at["mode"] == "links" and at["predicted_ms"] > 0
     assert at["plan"].split("+")[0] in ("uniform", "measured", "direct")
     assert at["candidates_predicted_ms"]["uniform"] > 0 and c["halo_route"]["link_cost"] in ("uniform", "measured")
+    # the ranks ran with enough hardware queues that no stream waits behind a peer-waiting kernel
+    assert int(c["gpu_max_hw_queues"]) >= 8
     # every halo row the timed rounds delivered equals its owner's row (2 ranks x 8 rows)
     assert c["halo_check"]["rows"] == 16 and c["halo_check"]["mismatches"] == 0
     # the host lane: probed with both ranks on it at once, offered to the plan, reported when used
