@@ -22,9 +22,10 @@ Cache is marked ``cache_reuse: true`` and also timed with its mixes in a scatter
 partly served by the cache and is not an HBM fraction. ``--devices-per-gpu L`` makes the weak
 form the headline (D = L*N).
 
-Each rank's population stacks are placement-calibrated before the timed region
-(``--placement-candidates``, federated_amd/placement.py: the fastest of 4 allocations per stack,
-probed with the same mix; the probe is reported in ``config.placement``).
+The headline runs on plain allocations, what every user of the library gets (round 6). At N = 1
+the same rounds are also timed on placement-calibrated stacks (``legs.placement_calibrated``,
+``--placement-leg``, federated_amd/placement.py: the fastest of 4 allocations per stack, probed
+with the same mix), reported beside the headline and never as ``value``.
 
 value = algorithmic bytes of all mixes on all ranks / max-over-ranks wall time, with
 algorithmic bytes = (K + 2) * P * 4 per device mix (K neighbour reads + local read + output
@@ -131,10 +132,13 @@ def parse():
                         "the buckets in pinned host memory, serial H2D + mix + D2H, chunk-pipelined, and "
                         "zero-copy over PCIe (reported under \"e2e\", never as value)")
     p.add_argument("--no-e2e", dest="e2e", action="store_false")
-    p.add_argument("--placement-candidates", type=int, default=4,
-                   help="allocate each population stack this many times and keep the fastest, timed "
-                        "with the population's own mix before the timed region (federated_amd/placement.py; "
-                        "1 = plain allocation)")
+    p.add_argument("--placement-candidates", type=int, default=1,
+                   help="the headline's stacks: allocate each population stack this many times and keep the "
+                        "fastest, timed with the population's own mix before the timed region "
+                        "(federated_amd/placement.py; 1 = plain allocation, the default: what users get)")
+    p.add_argument("--placement-leg", type=int, default=4,
+                   help="N = 1: also time the headline's rounds on stacks calibrated over this many candidates "
+                        "(legs.placement_calibrated; 0 or 1 = skip)")
     p.add_argument("--placement-release", action="store_true",
                    help="return the rejected placement candidates to the driver (then wait out its "
                         "background scrub) instead of leaving them in torch's caching allocator")
@@ -313,7 +317,10 @@ def child_command(argv, n: int, port: int, python: str = None) -> list:
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
-def child_env(base: dict, t0: float, status_file: str, ranks: int = 0) -> dict:
+def child_env(base: dict, t0: float, status_file: str) -> dict:
+    """The self-launched ranks' environment: the caller's, minus its rank variables, plus the run's
+    origin and status file. ``GPU_MAX_HW_QUEUES`` is left as the box exports it (round 6: nothing
+    in a round waits on a GPU queue any more, so the pool's 4 queues carry it)."""
     env = dict(base)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -321,54 +328,14 @@ def child_env(base: dict, t0: float, status_file: str, ranks: int = 0) -> dict:
     env[STATUS_FILE_ENV] = status_file
     env["PYTHONUNBUFFERED"] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this pool: dmabuf IPC only
-    set_hw_queues(env, ranks)  # the ranks are N > 1 processes
     return env
 
 
-HW_QUEUES = "8"           # ranks sharing a GPU (one-GPU rehearsals)
-HW_QUEUES_OWN_GPU = "16"  # one rank per GPU
-
-
-def visible_gpu_count(environ=None) -> int:
-    """GPUs this process could see, without loading HIP: the *_VISIBLE_DEVICES list when set, else
-    the KFD topology's GPU nodes (0 when neither can be read)."""
+def hw_queues_report(environ=None) -> str:
+    """``GPU_MAX_HW_QUEUES`` as the run sees it (never set by the bench)."""
     env = os.environ if environ is None else environ
-    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = env.get(k)
-        if v is not None and v.strip():
-            return len([x for x in v.split(",") if x.strip()])
-    base = "/sys/class/kfd/kfd/topology/nodes"
-    n = 0
-    try:
-        for d in os.listdir(base):
-            try:
-                with open(os.path.join(base, d, "gpu_id")) as fh:
-                    n += int(fh.read().strip() or "0") != 0
-            except (OSError, ValueError):
-                pass
-    except OSError:
-        return 0
-    return n
-
-
-def set_hw_queues(environ=None, ranks_here: int = 0) -> str:
-    """N > 1, before the HIP runtime loads: GPU_MAX_HW_QUEUES raised to at least 16 when each of the
-    node's ``ranks_here`` ranks has a GPU of its own, else 8 (a larger value is kept; the pool's
-    boxes export HIP's default of 4 explicitly). HIP maps
-    a process's streams onto that many hardware queues (4 by default) and streams beyond share one,
-    running in order: a kernel that waits for a peer (RCCL's, the host lane's wait kernel) then
-    holds back every stream on its queue, the compute stream included (`tools/probe/hw_queues.py`:
-    with 4 queues one of 7 streams stalled behind a parked wait, with 8 queues none of 9). A round
-    at N > 1 runs the compute, comm and two lane streams besides torch's own."""
-    env = os.environ if environ is None else environ
-    want = HW_QUEUES_OWN_GPU if 0 < ranks_here <= visible_gpu_count(env) else HW_QUEUES
-    try:
-        cur = int(env.get("GPU_MAX_HW_QUEUES", "0"))
-    except ValueError:
-        cur = 0
-    if cur < int(want):
-        env["GPU_MAX_HW_QUEUES"] = want
-    return env["GPU_MAX_HW_QUEUES"]
+    v = env.get("GPU_MAX_HW_QUEUES")
+    return v if v else "unset (HIP default 4)"
 
 
 def setup_rccl_diagnostics(rank: int, environ=None):
@@ -420,7 +387,7 @@ def self_launch(argv, n: int, total_seconds: float, grace: float = 120.0, python
     print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
     # the launcher stays in this process's group, so an outer time limit that signals the group
     # (coreutils timeout does) reaches every rank too
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file, n),
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=child_env(os.environ, t0, status_file),
                             text=True, bufsize=1)
     killed = threading.Event()
 
@@ -720,17 +687,11 @@ def seed_shard(shard, info, P):
     del full
 
 
-_COMM_STREAMS = {}
-
-
 def comm_stream():
-    """One exchange stream per device for the whole run (headline, decomposition, legs): every new
-    stream may take a hardware queue another active stream holds (``set_hw_queues``)."""
-    import torch
-    dev = torch.cuda.current_device()
-    if dev not in _COMM_STREAMS:
-        _COMM_STREAMS[dev] = torch.cuda.Stream()
-    return _COMM_STREAMS[dev]
+    """The run's one exchange stream on the current device (headline, decomposition, legs, link
+    probe): ``federated_amd.streams``, the rank's stream budget."""
+    from federated_amd.streams import role_stream
+    return role_stream("comm")
 
 
 def run_leg(args, shard, world, steps, warmup, timed_kernel=True):
@@ -978,6 +939,53 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
     }
 
 
+def lane_reserve_elems(world: int, devices: int, hl: int, hr: int, P: int, partition: str = "devices",
+                       dev_groups=None) -> int:
+    """The most elements the headline's route can put on the host lane for one (sender,
+    receiver) pair: the pair's whole halo demand (every plan's lane share is at most that). The lane
+    probe reserves and pins segments of this size, so a /dev/shm or pinning limit that would fail
+    the headline's lane fails the probe (and the lane is left out of the plan) instead."""
+    from federated_amd.halo import ring_transfers
+    from federated_amd.population import partition_shape, slice_bounds
+    gd, gp = partition_shape(partition, world, devices, dev_groups)
+    if gd < 2:
+        return 0
+    bounds = slice_bounds(P, gp)
+    demand = {}
+    for t in ring_transfers(gd, devices // gd, hl, hr, P, slice_world=gp, slice_bounds=bounds):
+        demand[(t.src, t.dst)] = demand.get((t.src, t.dst), 0) + (t.hi - t.lo)
+    return max(demand.values(), default=0)
+
+
+def headline_with_lane_fallback(measure, agree, lane: dict, probe: dict):
+    """N > 1: measure the exchanging headline (``measure()``, collective). If it fails on any rank
+    while the host lane was offered to its route (opening the lane, a lane wait that timed out, or
+    anything else in the build and its timed rounds), the lane's pseudo-links are dropped from
+    ``probe["plan_rates"]``, ``lane["error"]`` says why, and the same partition is measured again
+    without the lane: the ``devices`` headline is never lost to an optional path. Returns
+    (measure()'s result, None) or (None, the error) when the headline failed without the lane too
+    (the caller then falls back to ``params``). ``agree(ok)``: the control plane's all-ranks AND."""
+    from federated_amd.halo import is_lane_link
+
+    def attempt():
+        try:
+            return measure(), None
+        except Exception as exc:
+            return None, f"{type(exc).__name__}: {exc}"
+    res, err = attempt()
+    if agree(err is None):
+        return res, None
+    rates = probe.get("plan_rates") or {}
+    if not any(is_lane_link(l) for l in rates):
+        return None, err or "the headline failed on another rank"
+    lane["error"] = f"the headline with the host lane failed ({err or 'on another rank'}); measured without the lane"
+    probe["plan_rates"] = {l: r for l, r in rates.items() if not is_lane_link(l)}
+    res, err = attempt()
+    if agree(err is None):
+        return res, None
+    return None, err or "the headline failed on another rank"
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -994,8 +1002,6 @@ def main():
         wd = args.total_seconds + 90.0 if args.total_seconds > 0 else 900.0
     watchdog = Watchdog(wd, rank, t0)
     rccl_log = setup_rccl_diagnostics(rank) if world > 1 else None  # before anything opens RCCL
-    if world > 1:  # before torch loads the HIP runtime
-        set_hw_queues(ranks_here=int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     route_tune = "none" if args.no_autotune else args.route_tune
     if args.p2p_channels:
         os.environ["NCCL_NCHANNELS_PER_PEER"] = str(args.p2p_channels)
@@ -1019,6 +1025,7 @@ def main():
 
     from federated_amd.engine import get_engine
     from federated_amd.population import make_ring_shard, scattered_order
+    from federated_amd.streams import budget as stream_budget
 
     P, K = args.params, args.neighbours
     if K % 2:
@@ -1092,55 +1099,76 @@ def main():
     # The host lane (federated_amd/hostlane.py): with --route-tune links, its rates with every rank
     # using it at once are measured after the links and join the plan's rates, so choose_route
     # prices every plan with and without it. A token drawn by rank 0 names the shared segments.
-    lane = {"result": None, "error": None, "token": None, "opened": 0}
+    lane = {"result": None, "error": None, "token": None, "opened": 0, "numa_nodes": None}
     if (headline_exchanges and args.host_lane == "auto" and probe["plan_rates"] is not None
             and args.lane_probe_mb > 0):
         watchdog.enter("host lane probe")
         from federated_amd.hostlane import new_token
-        from federated_amd.linkprobe import probe_lane
+        from federated_amd.linkprobe import lane_pair_rates, probe_lane
+        # where every rank's GPU sits: a segment is placed on its receiver's NUMA node, and a
+        # cross-node pair is priced at its own probed rate (linkprobe.lane_pair_rates)
+        topo = [None] * world
+        dist.all_gather_object(topo, gpu_topology(device))
+        lane["topology"] = topo
+        lane["numa_nodes"] = [t.get("numa_node") for t in topo]
         tok = [new_token() if rank == 0 else None]
         dist.broadcast_object_list(tok, src=0)
         lane["token"] = tok[0]
         t_lane = time.perf_counter()
         try:
-            # a lane whose words never arrive on this node costs one 15 s timeout, then is left out
+            reserve = lane_reserve_elems(world, D, K // 2, K // 2, P, headline, args.device_groups)
+        except ValueError:  # a partition the headline itself will refuse (reported there)
+            reserve = 0
+        try:
+            # a lane whose words never arrive on this node costs one 15 s timeout, then is left out;
+            # its segments are as large as the headline's plan can need, so a /dev/shm or pinning
+            # limit shows here and not in the headline
             lane["result"] = probe_lane(rank, world, torch.device("cuda", device), tok[0] + "p", agree_all,
-                                        elems=int(args.lane_probe_mb * 1e6 / 4), timeout_s=15.0)
+                                        elems=int(args.lane_probe_mb * 1e6 / 4), timeout_s=15.0,
+                                        numa_nodes=lane["numa_nodes"], segment_elems=reserve)
         except Exception as exc:
             lane["error"] = f"{type(exc).__name__}: {exc}"
             print(f"[bench rank {rank}] host lane probe failed: {lane['error']}", file=sys.stderr, flush=True)
         if lane["result"] is not None:
             lane["result"]["wall_s"] = round(time.perf_counter() - t_lane, 2)
-            probe["plan_rates"] = {**probe["plan_rates"], **lane["result"]["rates"]}
-        topo = [None] * world
-        dist.all_gather_object(topo, gpu_topology(device))
-        lane["topology"] = topo
+            probe["plan_rates"] = {**probe["plan_rates"], **lane_pair_rates(lane["result"], lane["numa_nodes"])}
 
-    def lane_summary():
+    def lane_summary(xinfo=None):
         if args.host_lane == "off":
             return {"mode": "off"}
-        if lane["error"] is not None:
-            return {"error": lane["error"]}
         r = lane["result"]
-        if r is None:
+        if r is None and lane["error"] is None:
             return None
-        return {"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"], "message_MB": round(r["elems"] * 4 / 1e6, 1),
-                "chunk_MB": round(r["chunk_elems"] * 4 / 2**20, 2), "timing": r["timing"], "wall_s": r.get("wall_s"),
-                "topology": lane.get("topology")}
+        out = {"error": lane["error"], "topology": lane.get("topology"), "numa_nodes": lane.get("numa_nodes"),
+               "waits": "host (cfa_host_wait_word): no wait on a GPU queue"}
+        if r is not None:
+            out.update({"out_GBps": r["out_GBps"], "in_GBps": r["in_GBps"],
+                        "message_MB": round(r["elems"] * 4 / 1e6, 1),
+                        "reserved_MB_per_parity": round(r["segment_elems"] * 4 / 1e6, 1),
+                        "chunk_MB": round(r["chunk_elems"] * 4 / 2**20, 2), "timing": r["timing"],
+                        "wall_s": r.get("wall_s")})
+        if xinfo and xinfo.get("lane"):
+            out["pairs"] = xinfo["lane"].get("pairs_all")
+        return out
 
-    def build(partition, devices=None, relay=None):
+    def build(partition, devices=None, relay=None, placement=None):
         transport = tstate["transport"]
         shard, info = make_ring_shard(rank, world, devices or D, K // 2, K // 2, P, torch.device("cuda", device),
                                       transport,
                                       eng, partition=partition, dev_groups=args.device_groups,
                                       relay=(not args.no_relay) if relay is None else relay,
                                       staged=not args.no_stages, window_batch=args.window_batch,
-                                      placement_candidates=args.placement_candidates,
+                                      placement_candidates=(args.placement_candidates if placement is None
+                                                            else placement),
                                       placement_release=args.placement_release, link_rates=probe["plan_rates"],
                                       message_us=probe["message_us"],
                                       lane_token=f"{lane['token']}s{lane['opened']}" if lane["token"] else None,
-                                      lane_agree=agree_all)
+                                      lane_agree=agree_all, lane_numa_nodes=lane["numa_nodes"])
         lane["opened"] += 1
+        if world > 1 and info.get("lane") is not None:  # every rank's pairs, for config.host_lane
+            pairs = [None] * world
+            dist.all_gather_object(pairs, [dict(p, src=rank) for p in info["lane"]["pairs"]])
+            info["lane"]["pairs_all"] = [p for part in pairs for p in (part or [])]
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
@@ -1201,7 +1229,9 @@ def main():
         # would slow the timed rounds (federated_amd/placement.py)
         if t_dir < t_rel:
             tune["chosen"] = "direct"
+            xshard.close()  # the losing shard's lane: unpinned and unmapped
             return dshard, dinfo, tune
+        dshard.close()
         del dshard
         tune["chosen"] = "relayed"
         return xshard, xinfo, tune
@@ -1220,7 +1250,11 @@ def main():
         watchdog.enter(f"build {partition} shard")
         xshard, xinfo, xtune = build_tuned(partition)
         watchdog.enter("timed rounds")
-        return (xshard, xinfo, xtune) + run_leg(args, xshard, world, args.steps, args.warmup)
+        try:
+            return (xshard, xinfo, xtune) + run_leg(args, xshard, world, args.steps, args.warmup)
+        except BaseException:
+            xshard.close()  # a failed round: release its lane before any retry
+            raise
 
     t_head0 = time.perf_counter()
     if world == 1:
@@ -1231,16 +1265,19 @@ def main():
         # exchanges nothing, then measures the headline and the run exits 3, as for a transport
         # that cannot open. (A failure on some ranks only leaves the others inside a collective;
         # the watchdog ends that run.)
-        err = None
-        try:
-            res = measure_headline(headline)
-        except Exception as exc:
-            err = f"{type(exc).__name__}: {exc}"
-            tail = rccl_log_tail(rccl_log)
-            if tail:
-                err += f" [RCCL log: {tail}]"
-            print(f"[bench rank {rank}] {headline} headline failed: {err}", file=sys.stderr, flush=True)
-        if not agree_all(err is None):
+        def measure_logged():
+            try:
+                return measure_headline(headline)
+            except Exception as exc:
+                tail = rccl_log_tail(rccl_log)
+                print(f"[bench rank {rank}] {headline} headline failed: {type(exc).__name__}: {exc}",
+                      file=sys.stderr, flush=True)
+                if tail:
+                    raise RuntimeError(f"{type(exc).__name__}: {exc} [RCCL log: {tail}]") from exc
+                raise
+        # a failure with the host lane in the plan is retried without it before any fallback
+        res, err = headline_with_lane_fallback(measure_logged, agree_all, lane, probe)
+        if err is not None:
             if headline == "params":
                 raise RuntimeError(f"the params headline failed ({err or 'on another rank'})")
             headline_fallback = {"wanted": headline, "measured": "params",
@@ -1332,14 +1369,17 @@ def main():
                 if route else None,
                 "links": probe["summary"] if probe["error"] is None else {"error": probe["error"]},
                 "halo_check": halo_check,
-                "host_lane": lane_summary() if headline_exchanges else None,
+                "host_lane": lane_summary(info) if headline_exchanges else None,
                 "placement": info.get("placement"),
                 "halo_carved": info.get("halo_carved"),
                 "cache_reuse": reuse,
                 "gpus_visible": ndev,
                 "ranks_share_gpus": world > ndev,
                 "rccl_env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))},
-                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                "gpu_max_hw_queues": hw_queues_report(),
+                "streams": {"compute": "torch current stream",
+                            "roles": {str(d): r for d, r in stream_budget().items()},
+                            "waits": "none on a GPU queue (host lane: host-side waits)"},
                 "rccl_version": rccl_version() if world > 1 else None,
                 "parallelism": f"population-{info['partition']}{world}",
                 "rows_note": (f"each rank's rows are {shard_P(info, P)} elements, so a mix's {K + 1}-row window "
@@ -1400,6 +1440,7 @@ def main():
     pmc_est = 45.0
     reserve = 15.0 + (2 * pmc_est if live else 0.0)
     legs = {}
+    legs_n1 = {}
     leg_failed = False
 
     import threading
@@ -1431,6 +1472,36 @@ def main():
             wait_for_status(15.0)
         return code
     report_partial.done = False
+
+    # N = 1: the same rounds on placement-calibrated stacks (placement.calibrated_stacks: the fastest
+    # of --placement-leg allocations per stack), beside the plain-allocation headline; the headline's
+    # stacks are released first and the leg's candidates go back to the driver after it
+    if world == 1 and args.placement_leg > 1 and args.placement_candidates <= 1:
+        est = 2.5 * t_headline + 30.0
+        if budget.left() - reserve - 45.0 >= est:
+            watchdog.enter("placement-calibrated leg")
+            shard.close()
+            del shard
+            try:
+                cshard, cinfo = build(headline, placement=args.placement_leg)
+                cel, cdur, claunch = run_leg(args, cshard, world, args.steps, args.warmup)
+                cavg = sum(cdur) / max(1, len(cdur))
+                cach = per_launch_bytes / (cavg * 1e-3) / 1e9 if cavg > 0 else 0.0
+                legs_n1["placement_calibrated"] = {
+                    "value": round(bytes_total / cel / 1e9, 2), "ms_per_step": round(cel / args.steps * 1e3, 4),
+                    "avg_launch_ms": round(cavg, 5), "achieved": round(cach, 1),
+                    "frac": round(cach / HBM_PEAK_GBS, 4), "placement": cinfo.get("placement"),
+                    "note": "the headline's rounds on stacks chosen as the fastest of %d allocations each "
+                            "(federated_amd/placement.py); value is the plain-allocation figure" % args.placement_leg}
+                cshard.close()
+                del cshard
+            except Exception as exc:
+                legs_n1["placement_calibrated"] = {"error": f"{type(exc).__name__}: {exc}"}
+            torch.cuda.empty_cache()
+        else:
+            legs_n1["placement_calibrated"] = {"skipped": "budget", "estimate_s": round(est, 1)}
+        if rank == 0:
+            result["legs"] = legs_n1
 
     # N > 1: the headline round taken apart on the headline's own shard (exchange only, compute
     # only, the model's prediction), so a scaling result explains itself. Budget-gated (the
@@ -1467,8 +1538,7 @@ def main():
             result["config"]["halo_route"]["achieved_critical_ms"] = decomp.get("exchange_groups_ms_sum")
 
     if world > 1 and not args.no_extra_legs and not weak:
-        if shard.lane is not None:
-            shard.lane.close()
+        shard.close()
         del shard
         drop_cached()
         if rank == 0:
@@ -1547,8 +1617,8 @@ def main():
                 err = f"{type(exc).__name__}: {exc}"
                 print(f"[bench rank {rank}] {name} leg failed: {err}", file=sys.stderr, flush=True)
             finally:
-                if xshard is not None and xshard.lane is not None:
-                    xshard.lane.close()
+                if xshard is not None:
+                    xshard.close()
                 xshard = None
                 drop_cached()
             try:

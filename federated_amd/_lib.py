@@ -24,6 +24,7 @@ CFA_E_INVALID = -1
 CFA_E_HIP = -2
 CFA_E_RCCL = -3
 CFA_E_UNSUPPORTED = -4
+CFA_E_TIMEOUT = -5
 
 CFA_MAX_FANIN = 16
 CFA_UNIQUE_ID_BYTES = 128
@@ -58,7 +59,7 @@ SIGNATURES = {
     "cfa_wait_signal": (_c_int, [_c_void_p, ctypes.c_uint, _c_void_p, ctypes.c_longlong]),
     "cfa_host_register": (_c_int, [_c_void_p, _c_size_t]),
     "cfa_host_unregister": (_c_int, [_c_void_p]),
-    "cfa_stream_wait_word": (_c_int, [_c_void_p, ctypes.c_uint, ctypes.c_longlong, _c_void_p, _c_void_p]),
+    "cfa_host_wait_word": (_c_int, [_c_void_p, ctypes.c_uint, ctypes.c_longlong]),
     "cfa_memcpy_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,

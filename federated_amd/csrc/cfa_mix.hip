@@ -13,6 +13,7 @@
 // a tile is issued before its first use; the fan-in N is a template parameter so the fold is
 // fully unrolled.
 #include <chrono>
+#include <thread>
 
 #include "cfa_internal.h"
 
@@ -65,42 +66,32 @@ extern "C" int cfa_stream_signal(unsigned* word_dev, unsigned value, void* strea
   stream_signal_kernel<<<1, 1, 0, (hipStream_t)stream>>>(word_dev, value);
   return check_launch("stream_signal");
 }
-namespace {
-// One lane polls a 32-bit word (a pinned host word that another GPU's stream signals) until it
-// reaches `value` in sequence order, so the stream's later work (the host lane's H2D copy) starts
-// only after the producer's D2H copy has landed. A wave that has not seen the value after `ticks`
-// wall-clock ticks stores `value` into `status` and exits: every wave reaches an exit. Once a
-// wait of the stream has timed out (status set), later waits return at once, so a peer that never
-// comes costs one timeout, not one per chunk.
-__global__ void stream_wait_kernel(const unsigned* word, unsigned value, unsigned long long ticks,
-                                   unsigned* status) {
-  if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
-  const unsigned long long t0 = wall_clock64();
-  for (;;) {
-    const unsigned w = __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (static_cast<int>(w - value) >= 0) return;
-    if (wall_clock64() - t0 > ticks) {
-      __hip_atomic_store(status, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-}
-}  // namespace
-extern "C" int cfa_stream_wait_word(const unsigned* word_dev, unsigned value, long long timeout_us,
-                                    unsigned* status_dev, void* stream) {
-  if (!word_dev || !status_dev) return fail(CFA_E_INVALID, "null wait or status word");
+// The host lane's waits run on the host, never on a stream: a wait parked on the GPU holds every
+// stream that shares its hardware queue (4 per process by default), the compute stream included.
+// The calling thread polls the pinned word (acquire loads: the producer's release store made its
+// copy visible with it) until it reaches `value` in sequence order, spinning for the first
+// ~20 us and then sleeping in 20 us steps, and gives up after `timeout_us`; the caller then
+// enqueues the copy the word guards. No process-wide state.
+extern "C" int cfa_host_wait_word(const unsigned* word_host, unsigned value, long long timeout_us) {
+  if (!word_host) return fail(CFA_E_INVALID, "null wait word");
   if (timeout_us <= 0) return fail(CFA_E_INVALID, "timeout_us must be positive (got %lld)", timeout_us);
-  static int khz = 0;  // wall_clock64 rate; the same for every MI355X of a node
-  if (!khz) {
-    int dev = 0;
-    CFA_HIP_CHECK(hipGetDevice(&dev));
-    CFA_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-    if (khz <= 0) return fail(CFA_E_HIP, "device reports no wall-clock rate");
+  auto reached = [&] { return static_cast<int>(__atomic_load_n(word_host, __ATOMIC_ACQUIRE) - value) >= 0; };
+  if (reached()) return CFA_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto spin = std::chrono::microseconds(20), limit = std::chrono::microseconds(timeout_us);
+  for (unsigned i = 1;; ++i) {
+    if (reached()) return CFA_OK;
+    if ((i & 63) == 0) {
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt > limit) break;
+      if (dt > spin) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    } else {
+      __builtin_ia32_pause();
+    }
   }
-  const unsigned long long ticks = static_cast<unsigned long long>(timeout_us) * (unsigned long long)khz / 1000ull;
-  stream_wait_kernel<<<1, 1, 0, (hipStream_t)stream>>>(word_dev, value, ticks, status_dev);
-  return check_launch("stream_wait_word");
+  if (reached()) return CFA_OK;
+  return fail(CFA_E_TIMEOUT, "wait word holds %u after %lld us, expected %u", __atomic_load_n(word_host, __ATOMIC_ACQUIRE),
+              timeout_us, value);
 }
 extern "C" int cfa_host_register(void* host, size_t bytes) {
   if (!host || !bytes) return fail(CFA_E_INVALID, "null or empty host range");

@@ -36,7 +36,10 @@ This module spreads the halo over every link:
   and ``(LANE_IN, b)`` (b's H2D), each shared by all of that rank's lane pieces; with measured
   rates for them (``linkprobe.probe_lane``) the greedy puts on the lane what shortens the critical
   path. Lane messages never reach the transport (``rank_ops`` leaves them out; ``lane_ops`` lists
-  them).
+  them). A pair whose two GPUs sit on different NUMA nodes (``numa.py``) also has a rate of its
+  own: the pseudo-link ``(a, lane_pair(b))``, loaded only by that pair's lane pieces, priced at the
+  probed cross-socket rate (``linkprobe.lane_pair_rates``), so the greedy sheds lane pieces from
+  cross-socket pairs first.
 * **Messages.** Each piece is one contiguous element range, so a message is one RCCL
   send/recv of a plain buffer slice. Within a group, every rank lists its sends to a peer in the
   order of one global message list, and the peer lists its receives in that same order, so the
@@ -58,6 +61,7 @@ DIRECT = -1
 LANE = -2      # path id of the host lane
 LANE_OUT = -2  # pseudo endpoints of the lane in link keys: (a, LANE_OUT) is rank a's D2H,
 LANE_IN = -3   # (LANE_IN, b) is rank b's H2D
+LANE_PAIR = -16  # (a, LANE_PAIR - b): the lane path of pair a -> b alone (priced pairs only)
 
 
 def is_lane_link(link: Tuple[int, int]) -> bool:
@@ -65,14 +69,30 @@ def is_lane_link(link: Tuple[int, int]) -> bool:
     return link[0] < 0 or link[1] < 0
 
 
-def path_links(g: int, a: int, b: int, k: int) -> List[Tuple[int, int, int]]:
+def lane_pair(b: int) -> int:
+    """The pseudo endpoint of pair (a, b)'s own lane link: key (a, lane_pair(b))."""
+    return LANE_PAIR - int(b)
+
+
+def lane_pair_dst(e: int) -> Optional[int]:
+    """b for a pair endpoint lane_pair(b), else None."""
+    return LANE_PAIR - e if e <= LANE_PAIR else None
+
+
+def priced_pairs(keys) -> frozenset:
+    """The (a, b) pairs that have a lane pair link among ``keys`` (a cost or rate dict's keys)."""
+    return frozenset((a, lane_pair_dst(e)) for a, e in keys if a >= 0 and lane_pair_dst(e) is not None)
+
+
+def path_links(g: int, a: int, b: int, k: int, pairs: frozenset = frozenset()) -> List[Tuple[int, int, int]]:
     """The (group, from, to) links a piece of demand (g, a, b) loads on path k: the direct link;
-    the lane's two pseudo-links (same group: the lane streams are not ordered behind the groups);
-    or relay k's first hop in group g and second hop in group g + 1."""
+    the lane's two pseudo-links (same group: the lane streams are not ordered behind the groups),
+    plus the pair's own lane link when (a, b) is in ``pairs``; or relay k's first hop in group g
+    and second hop in group g + 1."""
     if k == DIRECT:
         return [(g, a, b)]
     if k == LANE:
-        return [(g, a, LANE_OUT), (g, LANE_IN, b)]
+        return [(g, a, LANE_OUT), (g, LANE_IN, b)] + ([(g, a, lane_pair(b))] if (a, b) in pairs else [])
     return [(g, a, k), (g + 1, k, b)]
 
 
@@ -120,11 +140,12 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
     then to the lower relay rank: integer arithmetic with a fixed order, so every rank computes
     the same routes. ``cost[(a, b)]`` (positive integers, default 1 for every link) scales a
     part's weight on link a->b: with costs proportional to 1 / measured rate the loads are times.
-    ``lane`` adds the host lane (path LANE: pseudo-links (a, LANE_OUT) and (LANE_IN, b), costs
-    from ``cost`` like any link). Returns ``shares[(g, a, b)]`` = [(path, n_units)], path =
+    ``lane`` adds the host lane (path LANE: pseudo-links (a, LANE_OUT) and (LANE_IN, b), and the
+    pair link (a, lane_pair(b)) when ``cost`` has one; costs from ``cost`` like any link). Returns ``shares[(g, a, b)]`` = [(path, n_units)], path =
     DIRECT, LANE or the relay rank, direct first, then the lane, then relays ascending, n_units
     summing to ``units``; and the link loads per group, ``{(g, a, b): weight}``."""
     c = (lambda a, b: 1) if not cost else (lambda a, b: int(cost.get((a, b), 1)))
+    pairs = priced_pairs(cost or {})
     load: Dict[Tuple[int, int, int], int] = defaultdict(int)
     gmax: Dict[int, int] = defaultdict(int)
     counts = {key: defaultdict(int) for key in demand}
@@ -139,12 +160,12 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
                 cands = [DIRECT] + ([LANE] if lane else []) + \
                     ([k for k in range(world) if k != a and k != b] if relay else [])
                 for k in cands:
-                    links = path_links(g, a, b, k)
+                    links = path_links(g, a, b, k, pairs)
                     delta = sum(max(0, load[l] + w * c(l[1], l[2]) - gmax[l[0]]) for l in links)
                     key_cost = (delta, max(load[l] + w * c(l[1], l[2]) for l in links), len(links), k)
                     if best_cost is None or key_cost < best_cost:
                         best, best_cost = k, key_cost
-                for l in path_links(g, a, b, best):
+                for l in path_links(g, a, b, best, pairs):
                     load[l] += w * c(l[1], l[2])
                     gmax[l[0]] = max(gmax[l[0]], load[l])
                 counts[key][best] += 1
@@ -160,11 +181,12 @@ def route_shares(world: int, demand: Dict[Tuple[int, int, int], int], units: int
 def _critical(shares, demand, cost=None) -> int:
     """Sum over groups of the busiest link's (cost-weighted) load for a set of shares."""
     load: Dict[Tuple[int, int, int], int] = defaultdict(int)
+    pairs = priced_pairs(cost or {})
     for (g, a, b), parts in shares.items():
         units = sum(n for _, n in parts) or 1
         for k, n in parts:
             w = demand[(g, a, b)] * n // units
-            for l in path_links(g, a, b, k):
+            for l in path_links(g, a, b, k, pairs):
                 load[l] += w * (int(cost.get((l[1], l[2]), 1)) if cost else 1)
     gmax: Dict[int, int] = defaultdict(int)
     for (g, _, _), w in load.items():
@@ -188,13 +210,16 @@ class RoutePlan:
 
     def __init__(self, world: int, transfers: Sequence[Transfer], relay: bool = True, units: int = 64,
                  align: int = ALIGN, link_cost: Optional[Dict[Tuple[int, int], int]] = None,
-                 lane: bool = False):
+                 lane: bool = False, lane_pairs=None):
         """``link_cost``: integer cost per element of each directed link (``link_costs_from_rates``;
         the lane's pseudo-links included when ``lane``); None = every link alike. ``lane`` offers
-        the host lane as a path (kept only where it shortens the critical path). Every rank must
-        pass the same costs (the digest covers the routes they produce)."""
+        the host lane as a path (kept only where it shortens the critical path). ``lane_pairs``:
+        the (a, b) pairs whose lane pieces also load their own pair link (cross-socket pairs with
+        a probed rate; default: the pairs ``link_cost`` prices). Every rank must pass the same
+        costs (the digest covers the routes they produce)."""
         self.world = int(world)
         self.link_cost = {k: int(v) for k, v in link_cost.items()} if link_cost else None
+        self.lane_pairs = frozenset(lane_pairs) if lane_pairs is not None else priced_pairs(self.link_cost or {})
         for k, v in (self.link_cost or {}).items():
             if v < 1:
                 raise ValueError(f"link cost must be a positive integer, got {k}: {v}")
@@ -242,6 +267,8 @@ class RoutePlan:
                     self.groups[g].append(Message(g, t.src, t.dst, t.src_key, x0, t.dst_key, x0, cnt, lane=True))
                     self.link_elems[(t.src, LANE_OUT)] += cnt
                     self.link_elems[(LANE_IN, t.dst)] += cnt
+                    if (t.src, t.dst) in self.lane_pairs:
+                        self.link_elems[(t.src, lane_pair(t.dst))] += cnt
                     continue
                 off = slot_use[(k, t.stage)]
                 slot_use[(k, t.stage)] = off + -(-cnt // self.align) * self.align
@@ -283,6 +310,15 @@ class RoutePlan:
     def lane_elems(self) -> int:
         return sum(m.count for g in self.groups for m in g if m.lane)
 
+    def lane_pair_elems(self) -> Dict[Tuple[int, int], int]:
+        """Lane elements per (sender, receiver) pair."""
+        out: Dict[Tuple[int, int], int] = defaultdict(int)
+        for g in self.groups:
+            for m in g:
+                if m.lane:
+                    out[(m.src, m.dst)] += m.count
+        return dict(out)
+
     def max_link_elems(self) -> int:
         return max(self.link_elems.values(), default=0)
 
@@ -296,6 +332,8 @@ class RoutePlan:
             elif lane:
                 load[(m.src, LANE_OUT)] += m.count
                 load[(LANE_IN, m.dst)] += m.count
+                if (m.src, m.dst) in self.lane_pairs:
+                    load[(m.src, lane_pair(m.dst))] += m.count
         return dict(load)
 
     def critical_elems(self) -> int:
@@ -425,7 +463,9 @@ class RoutedExchange:
         self.done = [plan.stages_done_after(g) for g in range(len(plan.groups))]
 
     def lane_event(self, stage: int):
-        """The last lane event at or before ``stage``'s group (None: nothing of it on the lane)."""
+        """The lane gate (``hostlane.LaneGate``: ``stream.wait_event(gate)`` pumps the lane on the
+        host until its pieces are enqueued, then waits for them) of the last group at or before
+        ``stage``'s group (None: nothing of it on the lane)."""
         pos = self.plan.stages.index(stage)
         best = None
         for g, e in self._lane_events.items():
@@ -441,6 +481,8 @@ class RoutedExchange:
         if self.lane is not None:
             self._lane_events = self.lane.run(stream, timing=lane_timing)
         for g, op in enumerate(self.ops):
+            if self.lane is not None:
+                self.lane.pump()
             if callable(op):
                 op(stream)
             else:
@@ -450,6 +492,12 @@ class RoutedExchange:
             if stage_done is not None:
                 for s in self.done[g]:
                     stage_done(s)
+
+    def finish_lane(self) -> None:
+        """Complete the round's host-lane part on the host (every H2D enqueued, ACKs raised); a
+        no-op without a lane. ``population`` calls it through ``wait_streams`` at the round's end."""
+        if self.lane is not None:
+            self.lane.finish()
 
 
 def link_costs_from_rates(rates_gbps: Dict[Tuple[int, int], float], scale: int = 16,
@@ -479,6 +527,8 @@ def _link_name(link: Tuple[int, int]) -> str:
         return f"{a}->host"
     if a == LANE_IN:
         return f"host->{b}"
+    if lane_pair_dst(b) is not None:
+        return f"{a}->host->{lane_pair_dst(b)}"
     return f"{a}->{b}"
 
 
@@ -501,6 +551,7 @@ def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
         return uniform, {"chosen": "uniform", "candidates": {}}
     lane_ok = any(is_lane_link(l) for l in rates_gbps)
     xgmi = {l: r for l, r in rates_gbps.items() if not is_lane_link(l)}
+    pairs = priced_pairs(rates_gbps)  # cross-socket lane pairs with a rate of their own
     costs = link_costs_from_rates(rates_gbps, tolerance=tolerance)
     msg = max(0.0, float(message_us or 0.0))
     cands = []
@@ -508,14 +559,15 @@ def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
         sfx = "+lane" if lane else ""
         for u in units:
             base = uniform if (u == units[0] and not lane) else \
-                RoutePlan(world, transfers, relay=relay, units=u, lane=lane)
+                RoutePlan(world, transfers, relay=relay, units=u, lane=lane, lane_pairs=pairs)
             tag = ("" if u == units[0] else f"/{u}") + sfx
             cands.append(("uniform" + tag, base))
             if costs and len(set(costs.values())) > 1:
                 cands.append(("measured" + tag, RoutePlan(world, transfers, relay=relay, link_cost=costs, units=u,
-                                                         lane=lane)))
+                                                         lane=lane, lane_pairs=pairs)))
             if base.relay:
-                cands.append(("direct" + tag, RoutePlan(world, transfers, relay=False, units=u, lane=lane)))
+                cands.append(("direct" + tag, RoutePlan(world, transfers, relay=False, units=u, lane=lane,
+                                                        lane_pairs=pairs)))
             if msg <= 0:
                 break  # without a per-message cost, fewer parts can only lengthen the critical path
     scored = [(p.predicted_ms(rates_gbps, message_us=msg, lane_chunk_bytes=lane_chunk_bytes), i, name, p)
@@ -523,6 +575,7 @@ def choose_route(world: int, transfers: Sequence[Transfer], relay: bool = True,
     best = min(scored, key=lambda x: (round(x[0], 9), x[1]))
     return best[3], {"chosen": best[2], "candidates": {name: round(t, 4) for t, _, name, _ in scored},
                      "message_us": round(msg, 2), "lane_offered": lane_ok,
+                     "lane_pairs_priced": sorted([a, b] for a, b in pairs),
                      "slow_links": sorted(_link_name(l) for l, c in costs.items() if c != 16 and l in xgmi)}
 
 

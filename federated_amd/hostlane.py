@@ -11,28 +11,36 @@ exchange models as files (TF1 ``cfa.py:119-130``).
 A lane piece (``halo.RoutePlan`` with ``lane=True``) goes:
 
     sender: D2H copy of the piece's chunk into the pair's shared segment  -> raise READY to its number
-    receiver: wait (on the GPU) until READY reaches that number  -> H2D copy into the halo row
+    receiver: its HOST sees READY reach that number  -> enqueues the H2D copy into the halo row
 
-Both ends are stream-ordered on the GPU: the sender's ``cfa_stream_signal`` (a one-lane
-system-scope release store into the pinned segment) follows its copy on the lane's out stream; the
-receiver's ``cfa_stream_wait_word`` (a one-lane kernel polling that word, with a timeout that
-every wave reaches) precedes its copy on the lane's in stream. The host only enqueues. Segments:
-one per (sender, receiver) pair that carries lane pieces, a POSIX shared-memory file created by the
-sender, mapped and pinned (``cfa_host_register``) by both, unlinked as soon as both hold it; two
-round parities of data, so the sender of round r waits only for the receiver's ACK of round
-r - 2. Chunks of ``chunk_elems`` keep D2H and H2D pipelined (a whole-row copy would serialise
-them).
+The sender's side is stream-ordered: ``cfa_stream_signal`` (a one-lane system-scope release store
+into the pinned segment) follows each D2H copy on the lane's out stream. The receiver's waits are
+on the host, never on a GPU queue (round 6): the thread that runs the round polls the word
+(``cfa_host_wait_word``, acquire loads) and only then enqueues the chunk's H2D on the lane's in
+stream. A wait parked on the GPU held every stream sharing its hardware queue (HIP maps a
+process's streams onto ``GPU_MAX_HW_QUEUES``, 4 on this pool), the compute stream included; a
+host wait holds nothing. The round's thread is also the pump: ``run`` enqueues the D2H side and
+returns; the H2D side is enqueued as the round consumes it (``pump`` between the interior mixes,
+non-blocking; a gate's ``wait(stream)`` before each boundary set, blocking until that set's
+chunks have arrived; ``finish`` at the round's end, which also raises the ACKs). A wait that
+times out raises in the round whose chunk it was, and the lane refuses every later round.
+
+Segments: one per (sender, receiver) pair that carries lane pieces, a POSIX shared-memory file
+created by the sender, its pages reserved with the policy "prefer the RECEIVER's NUMA node"
+(``numa.py``; the receiver's H2D reads local memory), mapped and pinned (``cfa_host_register``) by
+both, unlinked as soon as both hold it; two round parities of data, so the sender of round r waits
+(on the host) only for the receiver's ACK of round r - 2. Chunks of ``chunk_elems`` keep D2H and
+H2D pipelined (a whole-row copy would serialise them).
 
 The same protocol runs on CPU tensors (gloo tests): copies are ``torch`` copies between the
-segment and the buffers and the words are read and written by the host, so the cross-process
-protocol (layout, sequence numbers, parities, back-pressure) is tested without a GPU.
+segment and the buffers and the words are written by the host, so the cross-process protocol
+(layout, sequence numbers, parities, back-pressure, timeouts) is tested without a GPU.
 """
 from __future__ import annotations
 
 import ctypes
 import mmap
 import os
-import time
 from typing import Callable, Dict, Hashable, List, Optional, Sequence, Tuple
 
 import torch
@@ -47,6 +55,10 @@ DEFAULT_CHUNK_ELEMS = 8 << 20
 RAMP = 3  # a pair's round starts with chunks of 1/8, 1/4, 1/2 of that: the H2D starts after 4 MiB
 DEFAULT_TIMEOUT_S = 60.0
 SHM_DIR = "/dev/shm"
+
+
+class LaneTimeout(RuntimeError):
+    """A host-lane wait gave up: the peer's copy (or ACK) never arrived."""
 
 
 def lane_layout(msgs: Sequence[Message], align: int = ALIGN) -> Tuple[List[int], int]:
@@ -91,17 +103,23 @@ def segment_path(token: str, src: int, dst: int) -> str:
 class _Segment:
     """One direction's shared segment: [2 parities x ``elems`` fp32] then a flag page."""
 
-    def __init__(self, path: str, elems: int, create: bool):
+    def __init__(self, path: str, elems: int, create: bool, numa_node: Optional[int] = None):
         self.path, self.elems = path, int(elems)
         self.data_bytes = 2 * self.elems * 4
         self.size = self.data_bytes + FLAG_BYTES
+        self.numa_wanted = numa_node if create else None
+        self.numa_note = None
         flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
         fd = os.open(path, flags, 0o600)
         try:
             if create:
-                # reserve the pages now: a full /dev/shm fails here (ENOSPC, reported through the
-                # open's agreement) instead of a SIGBUS at the first copy into a sparse file
-                os.posix_fallocate(fd, 0, self.size)
+                # reserve the pages now, preferring the receiver's NUMA node: a full /dev/shm fails
+                # here (ENOSPC, reported through the open's agreement) instead of a SIGBUS at the
+                # first copy into a sparse file
+                from . import numa
+                with numa.preferred(numa_node) as why:
+                    self.numa_note = why
+                    os.posix_fallocate(fd, 0, self.size)
             self.mm = mmap.mmap(fd, self.size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
             os.close(fd)
@@ -111,6 +129,14 @@ class _Segment:
         self.data = torch.frombuffer(self.mm, dtype=torch.float32, count=2 * self.elems) if self.elems else None
         self.dev_base = None
         self._lib = None
+
+    def placed_nodes(self) -> List[Optional[int]]:
+        """NUMA node of the segment's first, middle and last data page (None: not known)."""
+        from . import numa
+        if not self.data_bytes:
+            return []
+        return [numa.node_of(self.base + off) for off in
+                sorted({0, self.data_bytes // 2 // 4096 * 4096, (self.data_bytes - 1) // 4096 * 4096})]
 
     def register(self, lib) -> None:
         from . import _lib
@@ -122,6 +148,9 @@ class _Segment:
 
     def host_ptr(self, parity: int, off: int) -> int:
         return self.base + (parity * self.elems + off) * 4
+
+    def word_host(self, i: int) -> int:
+        return self.base + self.data_bytes + 4 * i
 
     def word_dev(self, i: int) -> int:
         return self.dev_base + self.data_bytes + 4 * i
@@ -145,26 +174,59 @@ class _Segment:
 
 
 def _reached(word: int, value: int) -> bool:
-    """Sequence order of 32-bit counters (what the wait kernel tests: (int)(word - value) >= 0)."""
+    """Sequence order of 32-bit counters (what cfa_host_wait_word tests: (int)(word - value) >= 0)."""
     return ((word - value) & 0xFFFFFFFF) < 0x80000000
+
+
+class _Round:
+    """One round's state while the pump works through it."""
+
+    def __init__(self, r: int, timing: bool):
+        self.r, self.timing = r, timing
+        self.next = 0          # index of the next in-plan chunk to enqueue
+        self.events: Dict[int, object] = {}  # group -> event after its H2D copies (GPU)
+        self.ev: Dict[str, object] = {}      # timing events
+        self.done = False
+
+
+class LaneGate:
+    """What ``HostLane.run`` hands out per group: ``wait(stream)`` makes ``stream`` wait for the
+    group's lane pieces (and every earlier group's), pumping the lane on the host until they have
+    been enqueued; it is what ``torch.cuda.Stream.wait_event`` calls, so a gate stands where an
+    event would."""
+
+    def __init__(self, lane: "HostLane", rnd: _Round, group: int):
+        self.lane, self.rnd, self.group = lane, rnd, group
+
+    def wait(self, stream=None) -> None:
+        ev = self.lane.advance(self.group, self.rnd)
+        if ev is not None:
+            ev.wait(stream)
 
 
 class HostLane:
     """The host-lane messages of one rank, bound to its buffers and the pair segments.
 
     Build with ``HostLane.open`` (collective: every rank of the plan calls it). ``run(stream)``
-    issues one round's lane copies after ``stream``'s earlier work and returns
-    {group index: event after the H2D copies of that group's pieces} (GPU) or {} (CPU, where
-    ``run`` returns once every piece has landed)."""
+    starts one round after ``stream``'s earlier work and returns {group index: LaneGate};
+    ``pump()`` / a gate's ``wait`` / ``finish()`` enqueue the receiving side as its chunks arrive
+    (see the module docstring). On CPU tensors the copies happen at once, in the same calls."""
 
     def __init__(self, rank: int, sends: Sequence[Message], recvs: Sequence[Message],
                  buffers: Callable[[Hashable], torch.Tensor], device, token: str,
-                 chunk_elems: int = DEFAULT_CHUNK_ELEMS, timeout_s: float = DEFAULT_TIMEOUT_S):
+                 chunk_elems: int = DEFAULT_CHUNK_ELEMS, timeout_s: float = DEFAULT_TIMEOUT_S,
+                 numa_nodes: Optional[Sequence[Optional[int]]] = None, segment_elems: int = 0):
+        """``numa_nodes[r]``: the NUMA node of rank r's GPU (None or absent: no placement); the
+        segment a rank sends to r prefers r's node. ``segment_elems``: reserve at least this many
+        elements per parity of every segment (the lane probe reserves what the headline's plan
+        may need, so it fails where the headline would); both ends must pass the same value."""
         self.rank, self.token = int(rank), str(token)
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
         self.chunk_elems = max(ALIGN, int(chunk_elems) // ALIGN * ALIGN)
         self.timeout_s = float(timeout_s)
+        self.numa_nodes = list(numa_nodes) if numa_nodes is not None else None
+        self.segment_elems = max(0, int(segment_elems))
         self.round = 0
         self.out_msgs: Dict[int, List[Message]] = {}
         self.in_msgs: Dict[int, List[Message]] = {}
@@ -189,18 +251,26 @@ class HostLane:
         self.out_seg: Dict[int, _Segment] = {}
         self.in_seg: Dict[int, _Segment] = {}
         self._lib = None
-        self._status = None
+        self._cur: Optional[_Round] = None
+        self._error: Optional[str] = None
         self.last_timing = None
 
     # -- setup --------------------------------------------------------------------------------
     def _layout(self, msgs):
         offs, n = lane_layout(msgs)
-        return offs, n, lane_chunks(msgs, offs, self.chunk_elems)
+        return offs, max(n, self.segment_elems), lane_chunks(msgs, offs, self.chunk_elems)
+
+    def _node(self, r: int) -> Optional[int]:
+        if self.numa_nodes is None or not (0 <= r < len(self.numa_nodes)):
+            return None
+        n = self.numa_nodes[r]
+        return int(n) if n is not None and n >= 0 else None
 
     def create_segments(self) -> None:
         for dst, ms in sorted(self.out_msgs.items()):
             _, n, _ = self._layout(ms)
-            self.out_seg[dst] = _Segment(segment_path(self.token, self.rank, dst), n, create=True)
+            self.out_seg[dst] = _Segment(segment_path(self.token, self.rank, dst), n, create=True,
+                                         numa_node=self._node(dst))
 
     def open_segments(self) -> None:
         for src, ms in sorted(self.in_msgs.items()):
@@ -208,17 +278,13 @@ class HostLane:
             self.in_seg[src] = _Segment(segment_path(self.token, src, self.rank), n, create=False)
         if self.gpu:
             from . import _lib
+            from .streams import role_stream
             self._lib = _lib.load()
             for seg in list(self.out_seg.values()) + list(self.in_seg.values()):
                 seg.register(self._lib)
-            # [out-stream timeout, in-stream timeout]: written by the wait kernels that time out
-            self._status = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-            dp = ctypes.c_void_p()
-            _lib.check("cfa_host_device_pointer",
-                       self._lib.cfa_host_device_pointer(ctypes.c_void_p(self._status.data_ptr()), ctypes.byref(dp)))
-            self._status_dev = dp.value
-            self.out_stream = torch.cuda.Stream(self.device)
-            self.in_stream = torch.cuda.Stream(self.device)
+            # the process's two lane streams (streams.py): every lane of the run shares them
+            self.out_stream = role_stream("lane_out", self.device)
+            self.in_stream = role_stream("lane_in", self.device)
         self._plan_round()
 
     def unlink(self) -> None:
@@ -244,6 +310,7 @@ class HostLane:
             err = f"{type(exc).__name__}: {exc}"
         if not agree(err is None):
             lane.unlink()
+            lane.close()
             raise RuntimeError(f"host lane: creating the segments failed ({err or 'on another rank'})")
         try:
             lane.open_segments()
@@ -259,7 +326,6 @@ class HostLane:
     def _plan_round(self) -> None:
         """Per pair: the copies of a round in group order (the sender interleaves its peers group
         by group, so every receiver's early stages leave first)."""
-        self._out_plan = []  # (group, dst, chunk number, segment offset, source slice)
         per_dst = {}
         for dst, ms in self.out_msgs.items():
             offs, n, chunks = self._layout(ms)
@@ -276,6 +342,10 @@ class HostLane:
                               for k, (i, lo, c, so) in enumerate(chunks)]
         self._in_plan.sort(key=lambda x: (x[0], x[2], x[1]))
         self._groups = sorted({x[0] for x in self._in_plan})
+        # per group: the in-plan index after its last chunk (the plan is sorted by group)
+        self._group_end = {}
+        for i, x in enumerate(self._in_plan):
+            self._group_end[x[0]] = i + 1
 
     # -- one round -------------------------------------------------------------------------------
     @property
@@ -287,81 +357,150 @@ class HostLane:
         return sum(m.count for ms in self.in_msgs.values() for m in ms)
 
     def check(self) -> None:
-        """Raise if a wait of an earlier round timed out (GPU: the wait kernels' status words)."""
-        if self._status is not None:
-            st = self._status.tolist()
-            if any(st):
-                raise RuntimeError(f"host lane rank {self.rank}: a wait timed out after {self.timeout_s:.0f} s "
-                                   f"(out-stream status {st[0]}, in-stream status {st[1]}): the peer's "
-                                   "copies never landed")
+        """Raise if a round of this lane has failed (a wait timed out): the lane is unusable."""
+        if self._error is not None:
+            raise RuntimeError(f"host lane rank {self.rank}: {self._error}")
 
-    def run(self, stream=None, timing: bool = False) -> Dict[int, object]:
-        """One round's lane copies; see the class docstring. ``timing`` records HIP events at the
-        start and end of each stream's work (``last_timing``: out / in milliseconds, per-group in
-        arrival ms), for the bench's decomposition."""
+    def _wait(self, seg: _Segment, word: int, value: int, what: str, r: int) -> None:
+        """Host-side wait for ``seg``'s ``word`` to reach ``value``; a timeout fails round ``r``
+        here and now, and the lane with it."""
+        if _reached(seg.read(word), value):
+            return
+        from . import _lib
+        lib = self._lib or _lib.load()
+        rc = lib.cfa_host_wait_word(ctypes.c_void_p(seg.word_host(word)), value & 0xFFFFFFFF,
+                                    max(1, int(self.timeout_s * 1e6)))
+        if rc == _lib.CFA_OK:
+            return
+        msg = (f"round {r}: timed out after {self.timeout_s:g} s waiting for {what} (word {seg.read(word)}, "
+               f"want {value & 0xFFFFFFFF}); the round's lane rows are invalid")
+        if rc != _lib.CFA_E_TIMEOUT:
+            msg = f"round {r}: waiting for {what} failed ({_lib.load().cfa_last_error().decode()})"
+        self._error = msg
+        raise LaneTimeout(f"host lane rank {self.rank}: {msg}")
+
+    def run(self, stream=None, timing: bool = False) -> Dict[int, LaneGate]:
+        """Start one round: wait (host) for the ACKs of round r - 2, enqueue every D2H copy and
+        its READY signal on the out stream after ``stream``'s earlier work (the rows are final
+        before they leave, and the halo rows are no longer read when they are overwritten).
+        Finishes the previous round first if its caller did not. Returns {group: LaneGate}.
+        ``timing`` records HIP events at the start and end of each stream's work
+        (``timing_ms``)."""
         self.check()
+        if self._cur is not None:
+            self.finish()
         r = self.round
         self.round += 1
-        if not self.gpu:
-            self._run_cpu(r)
-            return {}
-        return self._run_gpu(r, stream, timing)
-
-    def _run_gpu(self, r: int, stream, timing: bool) -> Dict[int, object]:
-        from . import _lib
-        lib = self._lib
+        rnd = self._cur = _Round(r, timing and self.gpu)
         par = r & 1
-        tmo = int(self.timeout_s * 1e6)
-        os_, is_ = self.out_stream, self.in_stream
-        st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        os_.wait_stream(st)  # the rows are final before they leave
-        is_.wait_stream(st)  # the halo rows are no longer read when they are overwritten
-        osh, ish = ctypes.c_void_p(os_.cuda_stream), ctypes.c_void_p(is_.cuda_stream)
-        ev = None
-        if timing:
-            ev = {"o0": torch.cuda.Event(enable_timing=True), "o1": torch.cuda.Event(enable_timing=True),
-                  "i0": torch.cuda.Event(enable_timing=True), "i1": torch.cuda.Event(enable_timing=True)}
-            ev["o0"].record(os_)
-            ev["i0"].record(is_)
-        if r >= 2:  # the receiver has drained round r - 2 from this parity
-            for dst, seg in self.out_seg.items():
-                _lib.check("cfa_stream_wait_word", lib.cfa_stream_wait_word(
-                    ctypes.c_void_p(seg.word_dev(ACK)), (r - 1) & 0xFFFFFFFF, tmo, ctypes.c_void_p(self._status_dev),
-                    osh))
-        for g, dst, k, so, src in self._out_plan:
-            seg = self.out_seg[dst]
-            _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(ctypes.c_void_p(seg.host_ptr(par, so)),
-                                                               ctypes.c_void_p(src.data_ptr()), src.numel() * 4, osh))
-            seq = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
-            _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(READY)), seq, osh))
-        events = {}
-        last = {}
-        for i, (g, src_rank, k, so, dst) in enumerate(self._in_plan):
-            last[g] = i
-        for i, (g, src_rank, k, so, dst) in enumerate(self._in_plan):
+        try:
+            if self.gpu:
+                st = stream if stream is not None else torch.cuda.current_stream(self.device)
+                self.out_stream.wait_stream(st)
+                self.in_stream.wait_stream(st)
+                if rnd.timing:
+                    for k, s in (("o0", self.out_stream), ("i0", self.in_stream)):
+                        rnd.ev[k] = torch.cuda.Event(enable_timing=True)
+                        rnd.ev[k].record(s)
+            if r >= 2:  # the receiver has drained round r - 2 from this parity
+                for dst, seg in self.out_seg.items():
+                    self._wait(seg, ACK, r - 1, f"rank {dst}'s ack of round {r - 2}", r)
+            if self.gpu:
+                from . import _lib
+                lib, osh = self._lib, ctypes.c_void_p(self.out_stream.cuda_stream)
+                for g, dst, k, so, src in self._out_plan:
+                    seg = self.out_seg[dst]
+                    _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(
+                        ctypes.c_void_p(seg.host_ptr(par, so)), ctypes.c_void_p(src.data_ptr()), src.numel() * 4, osh))
+                    seq = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
+                    _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(READY)), seq,
+                                                                          osh))
+            else:
+                for g, dst, k, so, src in self._out_plan:
+                    seg = self.out_seg[dst]
+                    n = src.numel()
+                    seg.data[par * seg.elems + so: par * seg.elems + so + n].copy_(src)
+                    seg.words[READY] = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
+        except LaneTimeout:
+            raise
+        except Exception as exc:
+            self._error = f"round {r}: {type(exc).__name__}: {exc}"
+            raise
+        return {g: LaneGate(self, rnd, g) for g in self._groups}
+
+    def _advance_to(self, upto: int, block: bool) -> None:
+        rnd = self._cur
+        r, par = rnd.r, rnd.r & 1
+        if self.gpu:
+            from . import _lib
+            lib, ish = self._lib, ctypes.c_void_p(self.in_stream.cuda_stream)
+        while rnd.next < upto:
+            i = rnd.next
+            g, src_rank, k, so, dst = self._in_plan[i]
             seg = self.in_seg[src_rank]
             seq = (r * self._in_n[src_rank] + k + 1) & 0xFFFFFFFF
-            _lib.check("cfa_stream_wait_word", lib.cfa_stream_wait_word(
-                ctypes.c_void_p(seg.word_dev(READY)), seq, tmo, ctypes.c_void_p(self._status_dev + 4), ish))
-            if timing and i == 0:  # the first chunk has landed in host memory: the pipeline is full
-                ev["i_first"] = torch.cuda.Event(enable_timing=True)
-                ev["i_first"].record(is_)
-            _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(ctypes.c_void_p(dst.data_ptr()),
-                                                               ctypes.c_void_p(seg.host_ptr(par, so)), dst.numel() * 4,
-                                                               ish))
-            if last[g] == i:
-                e = torch.cuda.Event(enable_timing=timing)
-                e.record(is_)
-                events[g] = e
-        for src_rank, seg in self.in_seg.items():
-            _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(ACK)),
-                                                                  (r + 1) & 0xFFFFFFFF, ish))
-        if timing:
-            ev["o1"].record(os_)
-            ev["i1"].record(is_)
-            ev["groups"] = events
-        self.last_timing = ev
-        return events
+            if not _reached(seg.read(READY), seq):
+                if not block:
+                    return
+                self._wait(seg, READY, seq, f"chunk {k} of round {r} from rank {src_rank}", r)
+            n = dst.numel()
+            if self.gpu:
+                if rnd.timing and i == 0:  # the first chunk has landed in host memory: the pipeline is full
+                    rnd.ev["i_first"] = torch.cuda.Event(enable_timing=True)
+                    rnd.ev["i_first"].record(self.in_stream)
+                _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(ctypes.c_void_p(dst.data_ptr()),
+                                                                   ctypes.c_void_p(seg.host_ptr(par, so)), n * 4, ish))
+                if self._group_end[g] == i + 1:
+                    e = torch.cuda.Event(enable_timing=rnd.timing)
+                    e.record(self.in_stream)
+                    rnd.events[g] = e
+            else:
+                dst.copy_(seg.data[par * seg.elems + so: par * seg.elems + so + n])
+            rnd.next = i + 1
+
+    def pump(self) -> None:
+        """Enqueue the H2D copies of every chunk of the current round that has arrived, in plan
+        order, without waiting (between the interior mixes)."""
+        if self._cur is None or self._cur.done or self._error is not None:
+            return
+        self._advance_to(len(self._in_plan), block=False)
+
+    def advance(self, group: int, rnd: Optional[_Round] = None):
+        """Block (on the host) until every chunk of ``group`` and the groups before it has arrived
+        and its H2D is enqueued; the event after the group's copies (GPU) or None (CPU)."""
+        self.check()
+        rnd = rnd or self._cur
+        if rnd is None:
+            raise RuntimeError("host lane: no round in progress")
+        if rnd is self._cur and not rnd.done:
+            self._advance_to(self._group_end.get(group, 0), block=True)
+        return rnd.events.get(group)
+
+    def finish(self) -> None:
+        """Complete the current round on the host: enqueue every remaining H2D (waiting for its
+        chunk), then the ACK of every incoming segment on the in stream after them."""
+        rnd = self._cur
+        if rnd is None:
+            return
+        self.check()
+        self._advance_to(len(self._in_plan), block=True)
+        ack = (rnd.r + 1) & 0xFFFFFFFF
+        if self.gpu:
+            from . import _lib
+            lib, ish = self._lib, ctypes.c_void_p(self.in_stream.cuda_stream)
+            for src_rank, seg in self.in_seg.items():
+                _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(ACK)), ack, ish))
+            if rnd.timing:
+                for k, s in (("o1", self.out_stream), ("i1", self.in_stream)):
+                    rnd.ev[k] = torch.cuda.Event(enable_timing=True)
+                    rnd.ev[k].record(s)
+                rnd.ev["groups"] = dict(rnd.events)
+            self.last_timing = rnd.ev if rnd.timing else None
+        else:
+            for src_rank, seg in self.in_seg.items():
+                seg.words[ACK] = ack
+        rnd.done = True
+        self._cur = None
 
     def timing_ms(self) -> Optional[dict]:
         """After the stream has been synchronised: the last timed round's out-stream and
@@ -378,43 +517,17 @@ class HostLane:
         return out
 
     def wait_streams(self, stream) -> None:
-        """Make ``stream`` wait for this round's lane work (both directions)."""
+        """Finish the round on the host and make ``stream`` wait for its lane work (both
+        directions)."""
+        self.finish()
         if self.gpu:
             stream.wait_stream(self.out_stream)
             stream.wait_stream(self.in_stream)
 
-    def _spin(self, seg: _Segment, word: int, value: int, what: str) -> None:
-        t_end = time.monotonic() + self.timeout_s
-        n = 0
-        while not _reached(seg.read(word), value):
-            n += 1
-            if n > 64:
-                time.sleep(50e-6)
-            if time.monotonic() > t_end:
-                raise RuntimeError(f"host lane rank {self.rank}: timed out after {self.timeout_s:.0f} s waiting for "
-                                   f"{what} (word {seg.read(word)}, want {value})")
-
-    def _run_cpu(self, r: int) -> None:
-        par = r & 1
-        if r >= 2:
-            for dst, seg in self.out_seg.items():
-                self._spin(seg, ACK, (r - 1) & 0xFFFFFFFF, f"rank {dst}'s ack of round {r - 2}")
-        for g, dst, k, so, src in self._out_plan:
-            seg = self.out_seg[dst]
-            n = src.numel()
-            seg.data[par * seg.elems + so: par * seg.elems + so + n].copy_(src)
-            seg.words[READY] = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
-        for g, src_rank, k, so, dst in self._in_plan:
-            seg = self.in_seg[src_rank]
-            seq = (r * self._in_n[src_rank] + k + 1) & 0xFFFFFFFF
-            self._spin(seg, READY, seq, f"chunk {k} of round {r} from rank {src_rank}")
-            n = dst.numel()
-            dst.copy_(seg.data[par * seg.elems + so: par * seg.elems + so + n])
-        for src_rank, seg in self.in_seg.items():
-            seg.words[ACK] = (r + 1) & 0xFFFFFFFF
-
     def close(self) -> None:
-        """Drain the lane's streams, then unpin and drop the segments."""
+        """Drain the lane's streams, then unpin and drop the segments. A round still in progress
+        is abandoned (its peer's next wait times out)."""
+        self._cur = None
         if self.gpu and hasattr(self, "out_stream"):
             self.out_stream.synchronize()
             self.in_stream.synchronize()
@@ -422,10 +535,23 @@ class HostLane:
             seg.close()
         self.out_seg, self.in_seg = {}, {}
 
+    def pairs(self) -> List[dict]:
+        """Every pair this rank sends to: receiver, the NUMA nodes of both GPUs, the node the
+        segment's pages were placed on (first, middle, last data page) and why placement was not
+        applied, if it was not."""
+        out = []
+        for dst, seg in sorted(self.out_seg.items()):
+            placed = seg.placed_nodes() if seg.mm is not None else []
+            out.append({"dst": dst, "src_node": self._node(self.rank), "dst_node": self._node(dst),
+                        "placed_nodes": placed, "MB": round(seg.data_bytes / 1e6, 1),
+                        **({"numa_note": seg.numa_note} if seg.numa_note else {})})
+        return out
+
     def summary(self) -> dict:
         return {"token": self.token, "chunk_MB": round(self.chunk_elems * 4 / 2**20, 2),
                 "out_MB": round(self.elems_out * 4 / 1e6, 2), "in_MB": round(self.elems_in * 4 / 1e6, 2),
-                "peers_out": sorted(self.out_msgs), "peers_in": sorted(self.in_msgs)}
+                "peers_out": sorted(self.out_msgs), "peers_in": sorted(self.in_msgs),
+                "waits": "host (cfa_host_wait_word)", "pairs": self.pairs()}
 
 
 def new_token() -> str:

@@ -111,7 +111,11 @@ def probe_links(transport, rank: int, world: int, device=None, elems: int = 16 <
     elems = max(ALIGN, elems // ALIGN * ALIGN)
     send = torch.full((elems,), float(rank), dtype=torch.float32, device=dev)
     recv = torch.empty(elems, dtype=torch.float32, device=dev)
-    stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+    if dev.type == "cuda":
+        from .streams import role_stream
+        stream = role_stream("comm", dev)  # the halo's own exchange stream (streams.py)
+    else:
+        stream = None
     device_timing = dev.type == "cuda" and not getattr(transport, "host_staged", False)
     times = torch.zeros((2, world, world), dtype=torch.float64)
     piece = max(ALIGN, elems // max(1, pieces) // ALIGN * ALIGN) if pieces > 1 else 0
@@ -208,7 +212,8 @@ def agree_gloo(ok: bool, group=None) -> bool:
 
 
 def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elems: int = 64 << 20, reps: int = 3,
-               warmup: int = 1, chunk_elems: Optional[int] = None, timeout_s: float = 60.0) -> dict:
+               warmup: int = 1, chunk_elems: Optional[int] = None, timeout_s: float = 60.0,
+               numa_nodes=None, segment_elems: int = 0) -> dict:
     """The host lane's rates (``hostlane.py``) with every rank using it at once: rank a sends
     ``elems`` floats to rank a + 1 and receives as many from rank a - 1 over pinned shared host
     memory, D2H and H2D pipelined in chunks, ``reps`` timed rounds after ``warmup``: at world 2 the
@@ -218,9 +223,13 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
     the last H2D: the pipelined lane's steady rate, free of the ranks' start skew; the planner
     adds the pipeline's fill separately), medians over the reps, HIP events on the lane's streams
     (host clock on CPU tensors). Collective (``agree(ok)``: the control plane's all-ranks AND; a failure
-    on any rank raises on every rank). Returns {"rates":
+    on any rank raises on every rank). ``numa_nodes[r]``: rank r's GPU's NUMA node (segments are
+    placed on the receiver's, as the headline's are); ``segment_elems``: reserve and pin segments
+    of at least that many elements per parity (what the headline's plan may put on one pair), so
+    that the probe fails where the headline's lane would. Returns {"rates":
     {(a, LANE_OUT): GB/s, (LANE_IN, b): GB/s}, "out_GBps": [per rank], "in_GBps": [per rank],
-    "elems": elems, "chunk_elems": c}, identical on every rank (all-reduced)."""
+    "elems": elems, "chunk_elems": c, "pairs": [[a, a + 1] per rank], "numa_nodes"},
+    identical on every rank (all-reduced)."""
     import statistics
     import torch
     import torch.distributed as dist
@@ -236,13 +245,14 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
     msgs = [Message(0, a, (a + 1) % world, "send", 0, "recv", 0, elems, lane=True) for a in range(world)]
     lane = HostLane.open(rank, [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank],
                          lambda k: bufs[k], dev, token, agree, chunk_elems=chunk_elems or DEFAULT_CHUNK_ELEMS,
-                         timeout_s=timeout_s)
+                         timeout_s=timeout_s, numa_nodes=numa_nodes, segment_elems=segment_elems)
     gpu = dev.type == "cuda"
-    stream = torch.cuda.Stream(dev) if gpu else None
+    stream = torch.cuda.current_stream(dev) if gpu else None
     outs, ins, err = [], [], None
     try:
         for _ in range(warmup):
             lane.run(stream)
+            lane.finish()
         if gpu:
             torch.cuda.synchronize(dev)
         lane.check()
@@ -255,6 +265,7 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
             try:
                 t0 = time.perf_counter()
                 lane.run(stream, timing=gpu)
+                lane.finish()
                 if gpu:
                     torch.cuda.synchronize(dev)
                     tm = lane.timing_ms()
@@ -295,5 +306,43 @@ def probe_lane(rank: int, world: int, device, token: str, agree=agree_gloo, elem
             rates[(LANE_IN, a)] = in_r[a]
     del bufs
     return {"rates": rates, "out_GBps": [round(x, 2) for x in out_r], "in_GBps": [round(x, 2) for x in in_r],
-            "elems": elems, "chunk_elems": lane.chunk_elems,
+            "elems": elems, "chunk_elems": lane.chunk_elems, "segment_elems": max(elems, int(segment_elems)),
+            "pairs": [[a, (a + 1) % world] for a in range(world)],
+            "numa_nodes": list(numa_nodes) if numa_nodes is not None else None,
             "timing": "HIP events on the lane streams" if gpu else "host clock (CPU tensors)"}
+
+
+def lane_pair_rates(probe: dict, numa_nodes=None) -> dict:
+    """The planner's lane rates from ``probe_lane``'s result, priced by pair where the GPUs sit on
+    different NUMA nodes (a segment lives on its receiver's node, so a cross-node pair's D2H
+    crosses the socket link):
+
+    * a rank's pseudo-links (a, LANE_OUT) / (LANE_IN, a) take its probed rates, except that a
+      rank whose probe pair was cross-node takes the median out rate of the same-node probe pairs
+      (its own figure was the cross-socket one);
+    * every cross-node directed pair (a, b) gets its own link (a, lane_pair(b)) at the slowest out
+      rate the cross-node probe pairs measured.
+
+    Without node information, or with every rank on one node, the probe's rates unchanged."""
+    from .halo import LANE_OUT, lane_pair
+    rates = dict(probe["rates"])
+    nodes = list(numa_nodes) if numa_nodes is not None else probe.get("numa_nodes")
+    world = len(probe.get("out_GBps") or [])
+    if not nodes or world < 2 or len(nodes) < world or any(n is None or n < 0 for n in nodes[:world]):
+        return rates
+    cross = [a for a, b in probe.get("pairs", []) if nodes[a] != nodes[b]]
+    if not cross:
+        return rates
+    same = [a for a, b in probe.get("pairs", []) if nodes[a] == nodes[b] and (a, LANE_OUT) in rates]
+    x_rate = min(rates[(a, LANE_OUT)] for a in cross if (a, LANE_OUT) in rates)
+    if same:
+        import statistics
+        local = statistics.median(rates[(a, LANE_OUT)] for a in same)
+        for a in cross:
+            if (a, LANE_OUT) in rates:
+                rates[(a, LANE_OUT)] = local
+    for a in range(world):
+        for b in range(world):
+            if a != b and nodes[a] != nodes[b]:
+                rates[(a, lane_pair(b))] = x_rate
+    return rates

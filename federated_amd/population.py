@@ -277,8 +277,8 @@ class RingPopulationShard:
 
     def open_lane(self, token: str, agree, **kw) -> None:
         """Open the host lane of the route (collective: every rank of the plan calls it with the
-        same ``token``; ``agree(ok)`` is the control plane's all-ranks AND). A no-op for a route
-        without lane pieces anywhere."""
+        same ``token``; ``agree(ok)`` is the control plane's all-ranks AND; ``kw`` goes to
+        ``HostLane``, e.g. ``numa_nodes``). A no-op for a route without lane pieces anywhere."""
         route = self._route_plan
         if route is None or not route.lane:
             return
@@ -288,10 +288,20 @@ class RingPopulationShard:
         self._routed = None
 
     def exchange(self, stream=None) -> None:
-        """The whole halo exchange, issued on ``stream`` (synchronous for host transports)."""
+        """The whole halo exchange, issued on ``stream`` (synchronous for host transports; the host
+        lane's part is finished on the host before this returns)."""
         r = self.routed()
         if r is not None:
             r.run(stream)
+            r.finish_lane()
+
+    def close(self) -> None:
+        """Release the shard's host lane (unpin and unmap its segments); the stacks go with the
+        object. Every path that drops a shard with a lane calls this."""
+        if self.lane is not None:
+            self.lane.close()
+            self.lane = None
+            self._routed = None
 
     def mix_device(self, i: int, stream=None) -> None:
         fn = self._launch.get(i)
@@ -323,7 +333,9 @@ class RingPopulationShard:
         rows = [self.bucket((g0 + o) % p.D) for o in range(-p.hl, len(devs) + p.hr)]
         self.engine.mix_window([self.mixed[i] for i in devs], rows, [self.alphas] * len(devs), p.hl, p.hr, stream)
 
-    def _mix_set(self, devices: List[int], stream, timer=None) -> None:
+    def _mix_set(self, devices: List[int], stream, timer=None, between=None) -> None:
+        """Mix ``devices`` on ``stream``; ``between()`` (optional) after each launch (the host
+        lane's non-blocking pump, so an H2D whose chunk has arrived is enqueued at once)."""
         if self.window_batch:
             for run in self.window_passes(devices):
                 if timer:
@@ -331,6 +343,8 @@ class RingPopulationShard:
                 self.mix_window(run, stream)
                 if timer:
                     timer(run[-1], False)
+                if between:
+                    between()
             return
         for i in devices:
             if timer:
@@ -338,6 +352,8 @@ class RingPopulationShard:
             self.mix_device(i, stream)
             if timer:
                 timer(i, False)
+            if between:
+                between()
 
     def halo_check(self, gather, slice_lo: int = 0) -> Tuple[int, int]:
         """After an exchange: every halo row against the row its owner holds, by ``row_checksum``.
@@ -409,7 +425,8 @@ class RingPopulationShard:
                 events[stage] = ev
 
         routed.run(ms, landed)
-        self._mix_set(self.interior_order(), cs, timer)
+        pump = routed.lane.pump if routed.lane is not None else None
+        self._mix_set(self.interior_order(), cs, timer, pump)
         for stage, devs in sets:
             ev = events.get(stage)
             if ev is not None:
@@ -418,12 +435,15 @@ class RingPopulationShard:
                 cs.wait_stream(ms)
             lev = routed.lane_event(stage) if routed.lane is not None else None
             if lev is not None:
-                cs.wait_event(lev)
-            self._mix_set(devs, cs)
+                cs.wait_event(lev)  # a hostlane.LaneGate: pumps the lane on the host, then waits
+            self._mix_set(devs, cs, between=pump)
         if ms is not cs:
             cs.wait_stream(ms)  # the next round's exchange must not overwrite a halo still read
-        if routed.lane is not None and on_gpu:
-            routed.lane.wait_streams(cs)  # nor the lane's; and the rows have left before they change
+        if routed.lane is not None:
+            if on_gpu:
+                routed.lane.wait_streams(cs)  # nor the lane's; and the rows have left before they change
+            else:
+                routed.lane.finish()
 
     @property
     def bytes_per_round(self) -> int:
@@ -471,7 +491,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
                     dev_groups: Optional[int] = None, relay: bool = True, staged: bool = True,
                     window_batch: int = 0, dtype=torch.float32, placement_candidates: int = 0,
                     placement_release: bool = False, link_rates=None, message_us: float = 0.0,
-                    lane_token: Optional[str] = None, lane_agree=None, lane_chunk_elems: Optional[int] = None):
+                    lane_token: Optional[str] = None, lane_agree=None, lane_chunk_elems: Optional[int] = None,
+                    lane_numa_nodes=None):
     """The shard of global rank ``rank`` for a fixed population of ``devices`` ring devices
     (strong scaling: the population does not grow with ``world``).
 
@@ -488,7 +509,8 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     When ``link_rates`` also holds the host lane's pseudo-links (``linkprobe.probe_lane``) the lane
     is offered to the route too; if the chosen route uses it the shard's lane is opened here
     (collective: every rank passes the same ``lane_token`` and ``lane_agree``, the control plane's
-    all-ranks AND)."""
+    all-ranks AND; ``lane_numa_nodes[r]``: the NUMA node of rank r's GPU, where the segments rank
+    r receives are placed)."""
     from .halo import choose_route, ring_transfers
     gd, gp = partition_shape(partition, world, devices, dev_groups)
     d, p = divmod(rank, gp)
@@ -516,7 +538,7 @@ def make_ring_shard(rank: int, world: int, devices: int, hl: int, hr: int, P: in
     shard = RingPopulationShard(plan, Pr, device, transport, engine, dtype, window_batch, route=route, rank=rank,
                                 stacks=stacks, carve=stacks is not None)
     if route is not None and route.lane:
-        shard.open_lane(lane_token, lane_agree, chunk_elems=chunk)
+        shard.open_lane(lane_token, lane_agree, chunk_elems=chunk, numa_nodes=lane_numa_nodes)
     info = {"partition": partition, "device_groups": gd, "param_slices": gp,
             "slice": [bounds[p], bounds[p + 1]], "first_device": plan.first, "devices_per_rank": L,
             "placement": placement, "halo_carved": shard.carved}

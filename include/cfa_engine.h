@@ -104,7 +104,8 @@ enum {
   CFA_E_INVALID = -1,     /* bad argument (null pointer, negative size, bad mode) */
   CFA_E_HIP = -2,         /* HIP runtime error (launch, memcpy, device) */
   CFA_E_RCCL = -3,        /* RCCL error */
-  CFA_E_UNSUPPORTED = -4  /* feature not available in this build */
+  CFA_E_UNSUPPORTED = -4, /* feature not available in this build */
+  CFA_E_TIMEOUT = -5      /* a host-side wait gave up (cfa_host_wait_word) */
 };
 
 /* Mixing rules. */
@@ -253,16 +254,15 @@ CFA_API int cfa_wait_signal(const unsigned* word_host, unsigned value, void* str
  * D2H over the sender's PCIe link into shared pinned host memory and H2D over the receiver's,
  * beside the xGMI links. cfa_host_register / cfa_host_unregister pin (hipHostRegister, mapped and
  * portable) and release a caller-mapped host range, e.g. a shared-memory segment both ranks map.
- * cfa_stream_wait_word enqueues a one-lane kernel that polls the 32-bit word at `word_dev` (device
- * address of a pinned host word the other rank's stream raises with cfa_stream_signal) until it
- * reaches `value` in sequence order ((int)(word - value) >= 0); the stream's later work waits for
- * it. After `timeout_us` without it the kernel stores `value` into `status_dev` and exits, so no
- * wave spins forever: the caller checks the status word after the round. A wait that finds the
- * status word already set returns at once (one timeout per status word, not one per wait). */
+ * The sender raises a chunk's sequence number with cfa_stream_signal after its D2H copy (stream
+ * ordered); the receiver's HOST thread waits for it with cfa_host_wait_word and only then enqueues
+ * the H2D copy, so no wait ever parks on a GPU queue (a parked wait would hold every stream sharing
+ * its hardware queue). cfa_host_wait_word polls the host word (acquire loads) until it reaches
+ * `value` in sequence order ((int)(word - value) >= 0): it spins ~20 us, then sleeps in 20 us
+ * steps, and returns CFA_E_TIMEOUT after `timeout_us` (> 0) without it. Host only: no HIP call. */
 CFA_API int cfa_host_register(void* host, size_t bytes);
 CFA_API int cfa_host_unregister(void* host);
-CFA_API int cfa_stream_wait_word(const unsigned* word_dev, unsigned value, long long timeout_us,
-                                 unsigned* status_dev, void* stream);
+CFA_API int cfa_host_wait_word(const unsigned* word_host, unsigned value, long long timeout_us);
 
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.

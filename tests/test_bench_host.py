@@ -132,19 +132,24 @@ def test_child_env_sets_origin_and_status_and_drops_rank_vars():
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["OMP_NUM_THREADS"] == "16"
     assert env["PYTHONUNBUFFERED"] == "1"
     assert bench.child_env({}, 0.0, "x")["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
-    # N > 1 ranks get 8 hardware queues (streams blocked behind a peer wait otherwise) unless set
-    assert env["GPU_MAX_HW_QUEUES"] == "8"
-    assert bench.child_env({"GPU_MAX_HW_QUEUES": "16"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "16"
-    assert bench.child_env({"GPU_MAX_HW_QUEUES": "4"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "8"  # raised
-    e = {}
-    assert bench.set_hw_queues(e) == "8" and e == {"GPU_MAX_HW_QUEUES": "8"}
-    # one rank per GPU: 16 queues; ranks sharing a GPU (a one-GPU rehearsal): 8
-    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}) == 8
-    e = {"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7", "GPU_MAX_HW_QUEUES": "4"}
-    assert bench.set_hw_queues(e, ranks_here=8) == "16"
-    e = {"HIP_VISIBLE_DEVICES": "0", "GPU_MAX_HW_QUEUES": "4"}
-    assert bench.set_hw_queues(e, ranks_here=2) == "8"
-    assert bench.child_env({"HIP_VISIBLE_DEVICES": "0,1"}, 0.0, "x", ranks=2)["GPU_MAX_HW_QUEUES"] == "16"
+    # the box's hardware-queue setting is never overridden (round 6: no wait parks on a GPU queue)
+    assert "GPU_MAX_HW_QUEUES" not in env
+    assert bench.child_env({"GPU_MAX_HW_QUEUES": "4"}, 0.0, "x")["GPU_MAX_HW_QUEUES"] == "4"
+    assert not hasattr(bench, "set_hw_queues")
+    assert bench.hw_queues_report({"GPU_MAX_HW_QUEUES": "4"}) == "4"
+    assert bench.hw_queues_report({}) == "unset (HIP default 4)"
+
+
+def test_lane_reserve_covers_every_plan_share():
+    """The lane probe's reservation is the largest per-pair halo demand: N = 2 (both halos between
+    one pair) 8 rows, N >= 3 4 rows, params: nothing to exchange."""
+    import bench
+    P = 25_000_000
+    assert bench.lane_reserve_elems(2, 128, 4, 4, P) == 8 * P
+    assert bench.lane_reserve_elems(8, 128, 4, 4, P) == 4 * P
+    assert bench.lane_reserve_elems(4, 128, 4, 4, P, "params") == 0
+    from federated_amd.population import slice_bounds
+    assert bench.lane_reserve_elems(4, 128, 4, 4, P, "hybrid", 2) == 8 * slice_bounds(P, 2)[1]
 
 
 FAKE_TORCHRUN = r'''#!/usr/bin/env python3
@@ -322,3 +327,90 @@ def test_bench_parses_the_route_and_decomposition_flags(monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py", "--host-lane", "off", "--lane-probe-mb", "64"])
     a = bench.parse()
     assert a.host_lane == "off" and a.lane_probe_mb == 64.0
+
+
+def _lane_fallback_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from federated_amd import hostlane
+        from federated_amd.dist import TorchTransport
+        from federated_amd.halo import LANE_IN, LANE_OUT, is_lane_link
+        from federated_amd.linkprobe import agree_gloo
+        from federated_amd.population import make_ring_shard
+        tok = [hostlane.new_token() if rank == 0 else None]
+        dist.broadcast_object_list(tok, src=0)
+        rates = {(a, b): 50.0 for a in range(world) for b in range(world) if a != b}
+        rates.update({(a, LANE_OUT): 50.0 for a in range(world)})
+        rates.update({(LANE_IN, a): 50.0 for a in range(world)})
+        probe = {"plan_rates": rates}
+        lane = {"error": None}
+        D, P = 16, 4096 + 64
+        attempts = []
+        real_dir = hostlane.SHM_DIR
+
+        def measure():
+            # rank 1's first lane open cannot create its segments (no such directory): HostLane.open
+            # raises on every rank, as a full /dev/shm or a refused pin would in the headline
+            hostlane.SHM_DIR = "/nonexistent-cfa-lane" if (rank == 1 and not attempts) else real_dir
+            attempts.append(1)
+            shard, info = make_ring_shard(rank, world, D, 4, 4, P, "cpu", TorchTransport(), None,
+                                          link_rates=probe["plan_rates"], lane_token=f"{tok[0]}s{len(attempts)}",
+                                          lane_agree=agree_gloo, lane_chunk_elems=256)
+            for i in range(shard.plan.L):
+                shard.models[i] = torch.full((P,), float(shard.plan.first + i))
+            shard.exchange()
+            return shard, info
+        res, err = bench.headline_with_lane_fallback(measure, agree_gloo, lane, probe)
+        shard, info = res
+        ok = err is None and info["partition"] == "devices" and not info["route"]["lane"]
+        ok &= shard.lane is None and len(attempts) == 2
+        ok &= lane["error"] is not None and "host lane" in lane["error"]
+        ok &= not any(is_lane_link(k) for k in probe["plan_rates"])
+        for i in shard.plan.boundary():  # the lane-free exchange delivered the halo
+            g = shard.plan.first + i
+            ok &= all(float(s[0]) == float(j) for s, j in zip(shard.sources(i), shard.plan.neighbours(g)))
+        q.put((rank, bool(ok), lane["error"]))
+    except Exception as exc:
+        q.put((rank, False, f"{type(exc).__name__}: {exc}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_lane_failure_keeps_the_devices_headline():
+    """Round-5 review item 2: a host-lane open that fails on ONE rank costs the lane, not the
+    devices headline. headline_with_lane_fallback sees the failure on every rank (the open's
+    agreement), drops the lane's pseudo-links from the plan's rates, records the error
+    (config.host_lane.error) and measures the devices partition again without the lane."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35300 + (os.getpid() % 997)
+    procs = [ctx.Process(target=_lane_fallback_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, ok, msg = q.get(timeout=120)
+        res[r] = (ok, msg)
+    for p in procs:
+        p.join(timeout=30)
+    assert all(ok for ok, _ in res.values()), res
+    assert "creating the segments failed" in res[0][1]
+
+
+def test_lane_fallback_without_a_lane_reports_the_error():
+    """No lane in the plan: a failed headline is not retried (the caller falls back to params)."""
+    import bench
+    calls = []
+
+    def measure():
+        calls.append(1)
+        raise RuntimeError("rccl says no")
+    lane, probe = {"error": None}, {"plan_rates": {(0, 1): 50.0, (1, 0): 50.0}}
+    res, err = bench.headline_with_lane_fallback(measure, lambda ok: ok, lane, probe)
+    assert res is None and "rccl says no" in err and len(calls) == 1 and lane["error"] is None

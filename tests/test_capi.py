@@ -111,18 +111,55 @@ def test_host_lane_entry_points_validate_before_any_hip_call():
     from federated_amd import _lib
     word = (ctypes.c_uint * 2)(0, 0)
     addr = ctypes.addressof(word)
-    with pytest.raises(_lib.CFAError, match="null wait or status word"):
-        _lib.call("cfa_stream_wait_word", None, 1, 1000, addr, None)
-    with pytest.raises(_lib.CFAError, match="null wait or status word"):
-        _lib.call("cfa_stream_wait_word", addr, 1, 1000, None, None)
+    with pytest.raises(_lib.CFAError, match="null wait word"):
+        _lib.call("cfa_host_wait_word", None, 1, 1000)
     with pytest.raises(_lib.CFAError, match="timeout_us must be positive"):
-        _lib.call("cfa_stream_wait_word", addr, 1, 0, addr + 4, None)
+        _lib.call("cfa_host_wait_word", addr, 1, 0)
     with pytest.raises(_lib.CFAError, match="null or empty host range"):
         _lib.call("cfa_host_register", None, 4096)
     with pytest.raises(_lib.CFAError, match="null or empty host range"):
         _lib.call("cfa_host_register", addr, 0)
     with pytest.raises(_lib.CFAError, match="null host pointer"):
         _lib.call("cfa_host_unregister", None)
+
+
+def test_host_wait_word_release_timeout_and_wrap():
+    """cfa_host_wait_word (the host lane's receive-side wait, host only): returns once another
+    thread raises the word, in sequence order (a later value also releases it, across the 32-bit
+    wrap); gives up with CFA_E_TIMEOUT after its timeout; several threads may wait at once (no
+    process-wide state)."""
+    import ctypes
+    import threading
+    import time
+
+    from federated_amd import _lib
+    lib = _lib.load()
+    words = (ctypes.c_uint * 4)(0, 0, 0xFFFFFFFE, 0)
+    addr = ctypes.addressof(words)
+
+    def setter(i, v, delay):
+        time.sleep(delay)
+        words[i] = v
+
+    th = [threading.Thread(target=setter, args=(0, 9, 0.03)), threading.Thread(target=setter, args=(1, 4, 0.05))]
+    rcs = {}
+
+    def waiter(i, v):
+        rcs[i] = lib.cfa_host_wait_word(addr + 4 * i, v, 10_000_000)
+    ws = [threading.Thread(target=waiter, args=(0, 7)), threading.Thread(target=waiter, args=(1, 4))]
+    t0 = time.perf_counter()
+    for t in ws + th:
+        t.start()
+    for t in ws + th:
+        t.join()
+    assert rcs == {0: 0, 1: 0} and time.perf_counter() - t0 < 5.0  # 9 >= 7 in sequence order
+    words[2] = 3  # wrapped past 0xFFFFFFFE: 3 is "after" 0xFFFFFFFF
+    assert lib.cfa_host_wait_word(addr + 8, 0xFFFFFFFF, 1000) == 0
+    t0 = time.perf_counter()
+    rc = lib.cfa_host_wait_word(addr + 12, 1, 100_000)  # never raised
+    dt = time.perf_counter() - t0
+    assert rc == _lib.CFA_E_TIMEOUT and 0.09 < dt < 3.0
+    assert b"expected 1" in lib.cfa_last_error()
 
 
 def test_single_hip_runtime_in_process():

@@ -191,6 +191,12 @@ class RecordingLane:
         self.rounds += 1
         return {}
 
+    def pump(self):
+        pass
+
+    def finish(self):
+        self.finished = self.rounds
+
 
 def test_bench_plan_world8_with_the_host_lane(stub):
     """The bench's N = 8 plan with the host lane offered (every link alike: the planner keeps relays
@@ -215,7 +221,7 @@ def test_bench_plan_world8_with_the_host_lane(stub):
         shards.append(shard)
         comms.append(rc.comm)
         lanes.append(shard.lane)
-    assert all(ln.rounds == 1 for ln in lanes)
+    assert all(ln.rounds == 1 and ln.finished == 1 for ln in lanes)  # exchange() finishes the lane's round
     logs = [parse(read_log(stub, c)) for c in comms]
     n_lane = 0
     for r, shard in enumerate(shards):

@@ -1,16 +1,16 @@
 """The host lane on the GPU (federated_amd/hostlane.py): halo pieces over PCIe through pinned shared
-host memory, D2H and H2D ordered across processes by cfa_stream_signal / cfa_stream_wait_word.
+host memory; the sender's D2H raises a word with cfa_stream_signal, the receiver's host waits for
+it (cfa_host_wait_word) and only then enqueues the H2D, so no wait parks on a GPU queue.
 
-- The wait kernel: a word that never comes ends the wait after its timeout with the status word
-  set, and every later wait on that status returns at once; a word raised by another stream
-  releases it.
 - Two processes on the one GPU (the lane's mechanism is per process pair, whichever GPUs they
   drive): the ring population sharded in 2 device blocks, the route planned with equal xGMI and
   lane rates so half the halo takes the lane (the rest over torch.distributed/gloo), several rounds
   with the mixed models fed back, every device bit for bit equal to the unsharded oracle
-  trajectory (oracle/cfa_oracle.sequential_mix).
+  trajectory (oracle/cfa_oracle.sequential_mix); run at the box's own GPU_MAX_HW_QUEUES (4 on this
+  pool: round 6 no longer raises it).
+- A lane round whose peer is late does not hold the compute stream: mixes enqueued before the
+  round's receive side complete while the host waits for the peer.
 """
-import ctypes
 import os
 import time
 
@@ -19,44 +19,6 @@ import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
-
-
-def _dev_ptr(lib, t):
-    from federated_amd import _lib
-    dp = ctypes.c_void_p()
-    _lib.check("cfa_host_device_pointer", lib.cfa_host_device_pointer(ctypes.c_void_p(t.data_ptr()), ctypes.byref(dp)))
-    return dp.value
-
-
-def test_stream_wait_word_timeout_and_release(gpu):
-    from federated_amd import _lib
-    lib = _lib.load()
-    word = torch.zeros(16, dtype=torch.int32, pin_memory=True)
-    status = torch.zeros(16, dtype=torch.int32, pin_memory=True)
-    wd, sd = _dev_ptr(lib, word), _dev_ptr(lib, status)
-    s = torch.cuda.Stream()
-    sh = ctypes.c_void_p(s.cuda_stream)
-    t0 = time.monotonic()
-    _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(wd), 5, 200_000, ctypes.c_void_p(sd), sh))
-    _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(wd), 7, 20_000_000, ctypes.c_void_p(sd), sh))
-    s.synchronize()
-    dt = time.monotonic() - t0
-    assert int(status[0]) == 5  # the first wait timed out; the second returned at once
-    assert 0.15 < dt < 5.0
-    # released by a signal on another stream
-    status.zero_()
-    a, b = torch.cuda.Stream(), torch.cuda.Stream()
-    _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(wd), 9, 10_000_000, ctypes.c_void_p(sd),
-                                                ctypes.c_void_p(a.cuda_stream)))
-    marker = torch.zeros(1, device="cuda")
-    with torch.cuda.stream(a):
-        marker.fill_(1.0)  # after the wait on stream a
-    _lib.check("signal", lib.cfa_stream_signal(ctypes.c_void_p(wd), 9, ctypes.c_void_p(b.cuda_stream)))
-    a.synchronize()
-    b.synchronize()
-    assert int(status[0]) == 0 and int(word[0]) == 9 and float(marker.item()) == 1.0
-    with pytest.raises(RuntimeError):
-        _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(wd), 1, 0, ctypes.c_void_p(sd), sh))
 
 
 def _worker(rank, world, port, D, P, rounds, q):
@@ -92,6 +54,7 @@ def _worker(rank, world, port, D, P, rounds, q):
         torch.cuda.synchronize()
         shard.lane.check()
         out = {plan.first + i: shard.models[i].cpu().numpy() for i in range(plan.L)}
+        info["lane"]["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
         q.put((rank, out, info["route"]["lane"], info.get("lane")))
         shard.lane.close()
     except Exception as exc:  # reported by the parent
@@ -100,9 +63,8 @@ def _worker(rank, world, port, D, P, rounds, q):
         dist.destroy_process_group()
 
 
-def test_host_lane_two_processes_match_the_oracle(gpu, monkeypatch):
+def test_host_lane_two_processes_match_the_oracle(gpu):
     import torch.multiprocessing as mp
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")  # as bench.py's ranks (bench.set_hw_queues)
     from federated_amd.population import RingShardPlan
     from oracle.cfa_oracle import sequential_mix
     D, P, rounds, world = 16, 300_037, 3, 2
@@ -118,6 +80,7 @@ def test_host_lane_two_processes_match_the_oracle(gpu, monkeypatch):
             rank, out, used_lane, lane_info = q.get(timeout=100)
             assert not isinstance(out, str), f"rank {rank}: {out}"
             assert used_lane and lane_info["in_MB"] > 0 and lane_info["out_MB"] > 0
+            assert lane_info["hw_queues"] == os.environ.get("GPU_MAX_HW_QUEUES")  # the box's own setting
             got.update(out)
     finally:
         for p in procs:
@@ -131,3 +94,81 @@ def test_host_lane_two_processes_match_the_oracle(gpu, monkeypatch):
         cur = [sequential_mix(cur[g], [cur[j] for j in ring.neighbours(g)], alphas) for g in range(D)]
     for g in range(D):
         assert np.array_equal(got[g], cur[g]), g
+
+
+def _late_peer_worker(rank, port, q, delay_s):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from federated_amd.halo import Message
+        from federated_amd.hostlane import HostLane, new_token
+        from federated_amd.linkprobe import agree_gloo
+        tok = [new_token() if rank == 0 else None]
+        dist.broadcast_object_list(tok, src=0)
+        n = 1 << 22
+        bufs = {"send": torch.full((n,), float(rank + 1), device="cuda"), "recv": torch.zeros(n, device="cuda")}
+        msgs = [Message(0, a, 1 - a, "send", 0, "recv", 0, n, lane=True) for a in range(2)]
+        lane = HostLane.open(rank, [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank],
+                             lambda k: bufs[k], torch.device("cuda", 0), tok[0], agree_gloo,
+                             chunk_elems=1 << 20, timeout_s=30.0)
+        cs = torch.cuda.current_stream()
+        x = torch.randn(1 << 24, device="cuda")
+        torch.cuda.synchronize()
+        out = {}
+        if rank == 1:
+            time.sleep(delay_s)  # the peer is late: rank 0's receive side has nothing to copy yet
+        gates = lane.run(cs)
+        # compute enqueued AFTER the round started, on the stream the lane's copies follow: with the
+        # receive-side wait on the host, nothing on any GPU queue waits for the late peer
+        done = torch.cuda.Event()
+        for _ in range(20):
+            x.mul_(1.0001)
+        done.record(cs)
+        if rank == 0:
+            t0 = time.monotonic()
+            while not done.query() and time.monotonic() - t0 < 0.5 * delay_s:
+                time.sleep(0.005)
+            out["compute_done_while_peer_late"] = bool(done.query())
+            out["peer_arrived_by_then"] = _reached_word(lane)
+        cs.wait_event(gates[0])
+        lane.wait_streams(cs)
+        torch.cuda.synchronize()
+        out["rows_ok"] = float(bufs["recv"][0]) == float(2 - rank) and float(bufs["recv"][-1]) == float(2 - rank)
+        agree_gloo(True)
+        lane.close()
+        q.put((rank, out))
+    except Exception as exc:
+        q.put((rank, f"{type(exc).__name__}: {exc}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _reached_word(lane):
+    from federated_amd.hostlane import READY
+    return any(seg.read(READY) != 0 for seg in lane.in_seg.values())
+
+
+def test_late_peer_does_not_hold_the_compute_stream(gpu):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 34700 + (os.getpid() % 997)
+    procs = [ctx.Process(target=_late_peer_worker, args=(r, port, q, 4.0)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, out = q.get(timeout=100)
+            assert not isinstance(out, str), f"rank {r}: {out}"
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert res[0]["compute_done_while_peer_late"] and not res[0]["peer_arrived_by_then"]
+    assert res[0]["rows_ok"] and res[1]["rows_ok"]

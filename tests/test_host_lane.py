@@ -153,11 +153,19 @@ def _worker(rank, world, port, D, P, rounds, q, partition="devices", gd=None):
                            chunk_elems=64 * 1024)
         ok = set(probe["rates"]) == {(a, LANE_OUT) for a in range(world)} | {(LANE_IN, a) for a in range(world)}
         ok &= all(r > 0 for r in probe["rates"].values())
-        rates = _rates(world, 50.0, 50.0)
+        from federated_amd.linkprobe import lane_pair_rates
+        # a fake two-socket node: the first half of the ranks on NUMA node 0, the rest on node 1 (a
+        # node this container may not have: the placement is then skipped, and said so)
+        nodes = [0] * (world // 2) + [1] * (world - world // 2)
+        pr = dict(probe, out_GBps=[50.0] * world, rates={k: 50.0 for k in probe["rates"]})
+        rates = {**_rates(world, 50.0), **lane_pair_rates(pr, nodes)}
         shard, info = make_ring_shard(rank, world, D, 4, 4, P, "cpu", TorchTransport(), None, relay=True,
                                       partition=partition, dev_groups=gd,
                                       link_rates=rates, lane_token=tok[0], lane_agree=agree_gloo,
-                                      lane_chunk_elems=256)
+                                      lane_chunk_elems=256, lane_numa_nodes=nodes)
+        pairs = info["lane"]["pairs"]
+        ok &= all(p["src_node"] == nodes[rank] and p["dst_node"] == nodes[p["dst"]] for p in pairs)
+        ok &= all(len(p["placed_nodes"]) >= 1 for p in pairs)
         ok &= bool(info["route"]["lane"]) and "+lane" in info["route_choice"]["chosen"]
         if partition == "devices":
             ok &= bool(info["route"]["relay"]) == (world == 8)  # at 8 ranks relays and the lane together
@@ -214,7 +222,7 @@ def test_host_lane_rounds_gloo(world, D, partition, gd):
     assert res == {r: True for r in range(world)}
 
 
-def _absent_peer_worker(rank, world, port, q):
+def _absent_peer_worker(rank, world, port, q, stop_after):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -222,7 +230,7 @@ def _absent_peer_worker(rank, world, port, q):
         import time
 
         from federated_amd.halo import Message
-        from federated_amd.hostlane import HostLane, new_token
+        from federated_amd.hostlane import HostLane, LaneTimeout, new_token
         from federated_amd.linkprobe import agree_gloo
         tok = [new_token() if rank == 0 else None]
         dist.broadcast_object_list(tok, src=0)
@@ -231,13 +239,31 @@ def _absent_peer_worker(rank, world, port, q):
         lane = HostLane.open(rank, [m for m in msgs if m.src == rank], [m for m in msgs if m.dst == rank],
                              lambda k: bufs[k], "cpu", tok[0], agree_gloo, chunk_elems=1024, timeout_s=1.0)
         out = None
-        if rank == 0:  # rank 1 never sends: rank 0's receive times out, loudly and boundedly
+        if rank == 0:  # rank 1 stops sending after `stop_after` rounds: rank 0's NEXT round fails
+            for r in range(stop_after):
+                gates = lane.run()
+                gates[0].wait()  # what a boundary set does before it mixes
+                lane.finish()
+                if not torch.equal(bufs["recv"], torch.full((4096,), 1.0 + r)):
+                    out = f"round {r}: wrong rows"
             t0 = time.monotonic()
             try:
+                gates = lane.run()  # the send side does not wait for rank 1 (two parities)
+                gates[0].wait()     # the receive side does: this round raises, not the next
+                out = out or "no error"
+            except LaneTimeout as exc:
+                out = out or ("timeout" if f"round {stop_after}:" in str(exc) else str(exc), time.monotonic() - t0)
+            try:
                 lane.run()
-                out = "no error"
+                refused = False
             except RuntimeError as exc:
-                out = ("timeout" if "timed out" in str(exc) else str(exc), time.monotonic() - t0)
+                refused = f"round {stop_after}" in str(exc)
+            out = (out, refused) if isinstance(out, tuple) else out
+        else:
+            for r in range(stop_after):
+                bufs["send"].fill_(1.0 + r)
+                lane.run()
+                lane.finish()
         agree_gloo(True)
         lane.close()
         q.put((rank, out))
@@ -245,15 +271,56 @@ def _absent_peer_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_absent_peer_times_out_loudly():
+@pytest.mark.parametrize("stop_after", [0, 3])
+def test_absent_peer_fails_its_own_round_loudly(stop_after):
+    """Host-side waits (round 6): a chunk that never comes raises LaneTimeout in the round it
+    belongs to (the first round, or round 3 after three good ones), after about the lane's timeout,
+    and the lane refuses every later round."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 34100 + (os.getpid() % 997)
-    procs = [ctx.Process(target=_absent_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    port = 34100 + (os.getpid() % 997) + stop_after * 11
+    procs = [ctx.Process(target=_absent_peer_worker, args=(r, 2, port, q, stop_after)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=30)
-    kind, seconds = res[0]
+    (kind, seconds), refused = res[0]
     assert kind == "timeout" and 0.9 < seconds < 10.0
+    assert refused
+
+
+def test_two_socket_topology_sheds_cross_pairs():
+    """A fake two-socket node (ranks 0-3 on node 0, 4-7 on node 1): the lane probe's ring pairs
+    3 -> 4 and 7 -> 0 cross the socket link and measured 15 GB/s against 50 for the others.
+    lane_pair_rates gives ranks 3 and 7 the same-node rate on their own pseudo-links and every
+    cross-node pair a link of its own at 15 GB/s; choose_route then puts less on a cross-node
+    pair's lane than on a same-node pair's, and predicts a shorter exchange than when it prices
+    every pair at its sender's rate."""
+    from federated_amd.halo import lane_pair, priced_pairs
+    from federated_amd.linkprobe import lane_pair_rates
+    world = 8
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    out = [50.0] * world
+    out[3] = out[7] = 15.0
+    probe = {"rates": {**{(a, LANE_OUT): out[a] for a in range(world)}, **{(LANE_IN, a): 50.0 for a in range(world)}},
+             "out_GBps": out, "in_GBps": [50.0] * world, "pairs": [[a, (a + 1) % world] for a in range(world)]}
+    rates = lane_pair_rates(probe, nodes)
+    assert rates[(3, LANE_OUT)] == 50.0 and rates[(7, LANE_OUT)] == 50.0
+    assert rates[(3, lane_pair(4))] == 15.0 and rates[(0, lane_pair(7))] == 15.0 and (0, lane_pair(1)) not in rates
+    assert priced_pairs(rates) == {(a, b) for a in range(8) for b in range(8) if nodes[a] != nodes[b]}
+    assert lane_pair_rates(probe, [0] * world) == probe["rates"]  # one node: unchanged
+    assert lane_pair_rates(probe, None) == probe["rates"]
+    full = {**_rates(world, 50.0), **rates}
+    tr = ring_transfers(world, 16, 4, 4, 25_000_000)
+    plan, rep = choose_route(world, tr, rates_gbps=full, lane_chunk_bytes=4 << 20)
+    assert plan.lane and rep["lane_pairs_priced"]
+    per = plan.lane_pair_elems()
+    cross = [per.get((a, b), 0) for a, b in [(3, 4), (4, 3), (7, 0), (0, 7)]]
+    same = [per.get((a, (a + 1) % 8), 0) for a in (0, 1, 4, 5)] + [per.get((a, a - 1), 0) for a in (2, 1, 6, 5)]
+    assert max(cross) < min(same), (cross, same)
+    # the same probe priced per rank (round 5): ranks 3 and 7 slow on every pair
+    naive = {**_rates(world, 50.0), **probe["rates"]}
+    nplan, _ = choose_route(world, tr, rates_gbps=naive, lane_chunk_bytes=4 << 20)
+    assert plan.predicted_ms(full) <= nplan.predicted_ms(full) + 1e-9
+    _check_lane_pairing(plan)

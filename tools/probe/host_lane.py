@@ -13,8 +13,9 @@ under mixing load.
 ``--mode xproc`` (parent without GPU + two child processes on the visible GPU): the mechanism
 of the host lane across processes. A shared-memory segment per direction, pinned in both
 processes with cfa_host_register; each child is the producer of one direction (D2H chunk ->
-cfa_stream_signal raises the chunk's sequence number) and the consumer of the other
-(cfa_stream_wait_word on that number -> H2D chunk), two round parities of buffers with an ack word
+cfa_stream_signal raises the chunk's sequence number) and the consumer of the other (its host
+waits for that number with cfa_host_wait_word, then enqueues the H2D chunk; round 6: no wait on a
+GPU queue), two round parities of buffers with an ack word
 for back-pressure. Every round the consumer checks the landed rows bit for bit against the
 producer's pattern. On a one-GPU box both directions share the one PCIe link, so the rates are
 a lower bound for two GPUs.
@@ -193,9 +194,10 @@ def child(a):
         # producer: the round's tag in the first element of every chunk, then D2H chunk by chunk
         with torch.cuda.stream(ps):
             src[::chunk_elems] = float(r)
-        if r >= 2:  # back-pressure: the consumer has drained round r - 2 from this parity
-            _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(out_seg.word(16)), r - 1, tmo,
-                                                        ctypes.c_void_p(out_seg.word(32)), psh))
+        if r >= 2:  # back-pressure: the consumer has drained round r - 2 from this parity (host wait)
+            if lib.cfa_host_wait_word(ctypes.c_void_p(out_seg.word(16, dev=False)), r - 1, tmo) != 0:
+                print(json.dumps({"child": me, "round": r, "timeout": "ack"}), flush=True)
+                return 3
         for c in range(nch):
             lo = c * chunk_elems
             n = min(chunk_elems, total - lo)
@@ -208,8 +210,9 @@ def child(a):
         for c in range(nch):
             lo = c * chunk_elems
             n = min(chunk_elems, total - lo)
-            _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(in_seg.word(0)), r * nch + c + 1, tmo,
-                                                        ctypes.c_void_p(in_seg.word(48)), csh))
+            if lib.cfa_host_wait_word(ctypes.c_void_p(in_seg.word(0, dev=False)), r * nch + c + 1, tmo) != 0:
+                print(json.dumps({"child": me, "round": r, "timeout": f"chunk {c}"}), flush=True)
+                return 3
             _lib.check("memcpy", lib.cfa_memcpy_async(ctypes.c_void_p(dst.data_ptr() + lo * 4),
                                                       ctypes.c_void_p(in_seg.base + par * parity_bytes + lo * 4),
                                                       n * 4, csh))
@@ -217,10 +220,6 @@ def child(a):
         e1.record(cs)
         cs.synchronize()
         ps.synchronize()
-        if in_seg.read_word(48) or out_seg.read_word(32):
-            print(json.dumps({"child": me, "round": r, "timeout": True, "consumer_status": in_seg.read_word(48),
-                              "producer_status": out_seg.read_word(32)}), flush=True)
-            return 3
         exp = expect.clone()
         exp[::chunk_elems] = float(r)
         ok = bool(torch.equal(dst, exp))

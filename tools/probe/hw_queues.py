@@ -1,18 +1,19 @@
 #!/usr/bin/env python3
-"""Do two HIP streams of one process share a hardware queue (and so block each other)?
+"""Do the rank's streams hold each other back at the box's hardware-queue count?
 
-HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues per process (4 by default);
-streams beyond that share a queue, and a queue runs its packets in order. A kernel that waits
-(the host lane's cfa_stream_wait_word, or an RCCL kernel waiting for its peer) then also holds
-back every other stream on its queue. This probe creates ``--streams`` torch streams, parks a
-wait kernel on stream 0 (it waits for a pinned host word the host raises after ``--hold-ms``), and
-for every other stream launches a tiny kernel and times from its enqueue to its completion: a
-stream that shares stream 0's queue completes only after the word is raised. One JSON line:
-per stream, completed before the release (independent queue) or not (shared).
+HIP maps a process's streams onto at most GPU_MAX_HW_QUEUES hardware queues (4 on this pool);
+streams beyond that share a queue, and a queue runs its packets in order. Round 5 measured this
+with a wait kernel parked on one stream (`profiles/r05_hw_queues.jsonl`: at 4 queues one of 7
+streams stalled behind it) and raised the queue count; round 6 removed every wait from the GPU
+queues (the host lane waits on the host, federated_amd/hostlane.py) and runs at the pool's
+setting. What is left to check is whether ordinary work on one of the rank's streams delays a
+tiny kernel on another: for each pair (A, B) of the rank's stream budget (compute = torch's
+current stream, and federated_amd.streams' comm, lane_out, lane_in), a long piece of work goes on
+A (a 1 GiB H2D copy from pinned memory for the lane streams, ~20 ms; a chain of element-wise
+kernels of about as long for compute / comm), then a tiny kernel on B; B is independent when its
+kernel completes before A's work does. One JSON line.
 
-Usage (GPU box): [GPU_MAX_HW_QUEUES=n] python tools/probe/hw_queues.py [--streams 8]"""
-import argparse
-import ctypes
+Usage (GPU box): [GPU_MAX_HW_QUEUES=n] python tools/probe/hw_queues.py"""
 import json
 import os
 import sys
@@ -22,45 +23,48 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--streams", type=int, default=8)
-    ap.add_argument("--hold-ms", type=float, default=300.0)
-    a = ap.parse_args()
     import torch
-    from federated_amd import _lib
-    lib = _lib.load()
-    word = torch.zeros(16, dtype=torch.int32, pin_memory=True)
-    status = torch.zeros(16, dtype=torch.int32, pin_memory=True)
-
-    def dev(t):
-        p = ctypes.c_void_p()
-        _lib.check("ptr", lib.cfa_host_device_pointer(ctypes.c_void_p(t.data_ptr()), ctypes.byref(p)))
-        return p.value
-    wd, sd = dev(word), dev(status)
-    streams = [torch.cuda.Stream() for _ in range(a.streams)]
-    x = torch.zeros(1024, device="cuda")
+    from federated_amd.streams import role_stream
+    dev = torch.device("cuda", torch.cuda.current_device())
+    roles = {"compute": torch.cuda.current_stream(dev)}
+    for r in ("comm", "lane_out", "lane_in"):
+        roles[r] = role_stream(r, dev)
+    host = torch.empty(1 << 28, dtype=torch.float32, pin_memory=True)  # 1 GiB
+    big = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+    x = torch.zeros(1024, device=dev)
     torch.cuda.synchronize()
-    res = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "streams": a.streams, "shares_with_0": []}
-    for i in range(1, a.streams):
-        word.zero_()
-        _lib.check("wait", lib.cfa_stream_wait_word(ctypes.c_void_p(wd), 1, int(10e6), ctypes.c_void_p(sd),
-                                                    ctypes.c_void_p(streams[0].cuda_stream)))
-        time.sleep(0.01)  # the wait kernel is running
-        ev = torch.cuda.Event()
-        with torch.cuda.stream(streams[i]):
-            x.add_(1.0)
-            ev.record(streams[i])
-        t0 = time.perf_counter()
-        done_early = False
-        while time.perf_counter() - t0 < a.hold_ms * 1e-3:
-            if ev.query():
-                done_early = True
-                break
-            time.sleep(0.0005)
-        word[0] = 1  # release stream 0
-        torch.cuda.synchronize()
-        res["shares_with_0"].append({"stream": i, "independent": done_early})
-    res["shared_count"] = sum(1 for r in res["shares_with_0"] if not r["independent"])
+
+    def long_work(s, role):
+        with torch.cuda.stream(s):
+            if role.startswith("lane"):
+                big.copy_(host, non_blocking=True)
+            else:
+                for _ in range(12):
+                    big.mul_(1.0001)
+
+    res = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "pairs": []}
+    for a, sa in roles.items():
+        for b, sb in roles.items():
+            if a == b:
+                continue
+            done_a = torch.cuda.Event()
+            long_work(sa, a)
+            done_a.record(sa)
+            ev = torch.cuda.Event()
+            with torch.cuda.stream(sb):
+                x.add_(1.0)
+                ev.record(sb)
+            t0 = time.perf_counter()
+            first = None
+            while time.perf_counter() - t0 < 2.0:
+                qb, qa = ev.query(), done_a.query()
+                if qb or qa:
+                    first = "b" if qb and not qa else ("a" if qa and not qb else "both")
+                    break
+                time.sleep(0.0002)
+            torch.cuda.synchronize()
+            res["pairs"].append({"long_on": a, "tiny_on": b, "tiny_first": first == "b"})
+    res["held_back"] = [f"{p['tiny_on']} behind {p['long_on']}" for p in res["pairs"] if not p["tiny_first"]]
     print(json.dumps(res), flush=True)
 
 

@@ -90,8 +90,6 @@ def main():
     ap.add_argument("--jitter-ms", type=float, default=3.0)
     ap.add_argument("--wall-s", type=float, default=240.0)
     a = ap.parse_args()
-    from bench import set_hw_queues
-    set_hw_queues()  # the children: as bench.py's ranks (at least 8 hardware queues)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 36500 + os.getpid() % 997
