@@ -809,6 +809,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
             evs[0].record(comm)
             e0 = evs[0]
             routed.run(comm, group_done=lambda g: evs[g + 1].record(comm), lane_timing=lane is not None)
+            routed.finish_lane()  # the pump has enqueued the round's H2D side (and its timing events)
         else:
             torch.cuda.synchronize()
             e0 = torch.cuda.Event(enable_timing=True)
@@ -819,6 +820,7 @@ def decompose_round(shard, world: int, steps: int, warmup: int, head_avg_ms: flo
                 torch.cuda.synchronize()
                 evs.append(time.perf_counter())
             routed.run(comm, group_done=done, lane_timing=lane is not None)
+            routed.finish_lane()
         if record:
             marks.append(evs)
             if lane is not None:

@@ -48,6 +48,13 @@ _c_int64_p = ctypes.POINTER(ctypes.c_int64)
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _PP = ctypes.POINTER(ctypes.c_void_p)  # float* const* (host table of device pointers)
 
+
+class LaneOp(ctypes.Structure):
+    """cfa_lane_op (include/cfa_engine.h): one operation of a host-lane pump round."""
+    _fields_ = [("wait_word", ctypes.c_void_p), ("wait_value", ctypes.c_uint), ("signal_value", ctypes.c_uint),
+                ("signal_word", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("src", ctypes.c_void_p),
+                ("bytes", ctypes.c_size_t), ("event", ctypes.c_void_p), ("mark", ctypes.c_int)]
+
 # name -> (restype, argtypes); mirrors include/cfa_engine.h one for one.
 SIGNATURES = {
     "cfa_version": (_c_int, []),
@@ -60,6 +67,10 @@ SIGNATURES = {
     "cfa_host_register": (_c_int, [_c_void_p, _c_size_t]),
     "cfa_host_unregister": (_c_int, [_c_void_p]),
     "cfa_host_wait_word": (_c_int, [_c_void_p, ctypes.c_uint, ctypes.c_longlong]),
+    "cfa_lane_pump_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_void_p, _c_int, _c_int]),
+    "cfa_lane_pump_submit": (_c_int, [_c_void_p, _c_void_p, _c_int, ctypes.c_longlong]),
+    "cfa_lane_pump_wait": (_c_int, [_c_void_p, _c_int, ctypes.c_longlong]),
+    "cfa_lane_pump_destroy": (_c_int, [_c_void_p]),
     "cfa_memcpy_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "cfa_mix_seq_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t, _c_void_p]),
     "cfa_mix_seq_ex_f32": (_c_int, [_c_void_p, _c_void_p, _PP, _c_float_p, _c_int, _c_size_t,

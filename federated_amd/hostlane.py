@@ -15,15 +15,17 @@ A lane piece (``halo.RoutePlan`` with ``lane=True``) goes:
 
 The sender's side is stream-ordered: ``cfa_stream_signal`` (a one-lane system-scope release store
 into the pinned segment) follows each D2H copy on the lane's out stream. The receiver's waits are
-on the host, never on a GPU queue (round 6): the thread that runs the round polls the word
-(``cfa_host_wait_word``, acquire loads) and only then enqueues the chunk's H2D on the lane's in
-stream. A wait parked on the GPU held every stream sharing its hardware queue (HIP maps a
+on the host, never on a GPU queue (round 6): a native pump thread of the lane's own
+(``cfa_lane_pump_*``, csrc/cfa_lane.cpp) polls each chunk's word (acquire loads) and only then
+enqueues the chunk's H2D on the lane's in stream, then the group's event, and at the round's end
+the ACKs. A wait parked on the GPU held every stream sharing its hardware queue (HIP maps a
 process's streams onto ``GPU_MAX_HW_QUEUES``, 4 on this pool), the compute stream included; a
-host wait holds nothing. The round's thread is also the pump: ``run`` enqueues the D2H side and
-returns; the H2D side is enqueued as the round consumes it (``pump`` between the interior mixes,
-non-blocking; a gate's ``wait(stream)`` before each boundary set, blocking until that set's
-chunks have arrived; ``finish`` at the round's end, which also raises the ACKs). A wait that
-times out raises in the round whose chunk it was, and the lane refuses every later round.
+host wait holds nothing, and on its own thread it does not hold the round's thread either (which
+may be inside a blocking transport call). ``run`` enqueues the D2H side and submits the receive
+side to the pump; before each boundary set a gate's ``wait(stream)`` blocks until the pump has
+enqueued that set's chunks and then makes the stream wait on their event; ``finish`` waits for the
+whole round. A wait that times out fails the round whose chunk it was (``LaneTimeout``), and the
+lane refuses every later round.
 
 Segments: one per (sender, receiver) pair that carries lane pieces, a POSIX shared-memory file
 created by the sender, its pages reserved with the policy "prefer the RECEIVER's NUMA node"
@@ -32,9 +34,10 @@ both, unlinked as soon as both hold it; two round parities of data, so the sende
 (on the host) only for the receiver's ACK of round r - 2. Chunks of ``chunk_elems`` keep D2H and
 H2D pipelined (a whole-row copy would serialise them).
 
-The same protocol runs on CPU tensors (gloo tests): copies are ``torch`` copies between the
-segment and the buffers and the words are written by the host, so the cross-process protocol
-(layout, sequence numbers, parities, back-pressure, timeouts) is tested without a GPU.
+The same protocol runs on CPU tensors (gloo tests): the send side's copies are ``torch`` copies
+and its words host stores, and the receive side runs on the same native pump in host mode
+(memcpy, host stores), so the cross-process protocol (layout, sequence numbers, parities,
+back-pressure, timeouts) is tested without a GPU.
 """
 from __future__ import annotations
 
@@ -183,7 +186,7 @@ class _Round:
 
     def __init__(self, r: int, timing: bool):
         self.r, self.timing = r, timing
-        self.next = 0          # index of the next in-plan chunk to enqueue
+        self.ops = None        # the pump's operation array (kept alive for the round)
         self.events: Dict[int, object] = {}  # group -> event after its H2D copies (GPU)
         self.ev: Dict[str, object] = {}      # timing events
         self.done = False
@@ -251,6 +254,7 @@ class HostLane:
         self.out_seg: Dict[int, _Segment] = {}
         self.in_seg: Dict[int, _Segment] = {}
         self._lib = None
+        self._pump = None
         self._cur: Optional[_Round] = None
         self._error: Optional[str] = None
         self.last_timing = None
@@ -276,15 +280,21 @@ class HostLane:
         for src, ms in sorted(self.in_msgs.items()):
             _, n, _ = self._layout(ms)
             self.in_seg[src] = _Segment(segment_path(self.token, src, self.rank), n, create=False)
+        from . import _lib
+        self._lib = _lib.load()
         if self.gpu:
-            from . import _lib
             from .streams import role_stream
-            self._lib = _lib.load()
             for seg in list(self.out_seg.values()) + list(self.in_seg.values()):
                 seg.register(self._lib)
             # the process's two lane streams (streams.py): every lane of the run shares them
             self.out_stream = role_stream("lane_out", self.device)
             self.in_stream = role_stream("lane_in", self.device)
+        pump = ctypes.c_void_p()
+        _lib.check("cfa_lane_pump_create", self._lib.cfa_lane_pump_create(
+            ctypes.byref(pump), ctypes.c_void_p(self.in_stream.cuda_stream if self.gpu else 0),
+            (self.device.index if self.device.index is not None else torch.cuda.current_device()) if self.gpu else 0,
+            0 if self.gpu else 1))
+        self._pump = pump
         self._plan_round()
 
     def unlink(self) -> None:
@@ -421,6 +431,7 @@ class HostLane:
                     n = src.numel()
                     seg.data[par * seg.elems + so: par * seg.elems + so + n].copy_(src)
                     seg.words[READY] = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
+            self._submit_receive(rnd)
         except LaneTimeout:
             raise
         except Exception as exc:
@@ -428,77 +439,89 @@ class HostLane:
             raise
         return {g: LaneGate(self, rnd, g) for g in self._groups}
 
-    def _advance_to(self, upto: int, block: bool) -> None:
-        rnd = self._cur
+    def _event(self, timing: bool):
+        """A HIP event the pump records: created (by a first record on the in stream, before the
+        round's operations) so that its handle exists and torch knows it was recorded."""
+        e = torch.cuda.Event(enable_timing=timing)
+        e.record(self.in_stream)
+        return e
+
+    def _submit_receive(self, rnd: _Round) -> None:
+        """The round's receive side as pump operations: per chunk, wait for its READY number, copy
+        it H2D (after the first chunk's wait, a timing event: the pipeline is full), the group's
+        event and progress mark after a group's last chunk; then every incoming segment's ACK, and
+        the in stream's end event when timed."""
+        from . import _lib
         r, par = rnd.r, rnd.r & 1
-        if self.gpu:
-            from . import _lib
-            lib, ish = self._lib, ctypes.c_void_p(self.in_stream.cuda_stream)
-        while rnd.next < upto:
-            i = rnd.next
-            g, src_rank, k, so, dst = self._in_plan[i]
+        ops = []
+        for i, (g, src_rank, k, so, dst) in enumerate(self._in_plan):
             seg = self.in_seg[src_rank]
             seq = (r * self._in_n[src_rank] + k + 1) & 0xFFFFFFFF
-            if not _reached(seg.read(READY), seq):
-                if not block:
-                    return
-                self._wait(seg, READY, seq, f"chunk {k} of round {r} from rank {src_rank}", r)
-            n = dst.numel()
-            if self.gpu:
-                if rnd.timing and i == 0:  # the first chunk has landed in host memory: the pipeline is full
-                    rnd.ev["i_first"] = torch.cuda.Event(enable_timing=True)
-                    rnd.ev["i_first"].record(self.in_stream)
-                _lib.check("cfa_memcpy_async", lib.cfa_memcpy_async(ctypes.c_void_p(dst.data_ptr()),
-                                                                   ctypes.c_void_p(seg.host_ptr(par, so)), n * 4, ish))
-                if self._group_end[g] == i + 1:
-                    e = torch.cuda.Event(enable_timing=rnd.timing)
-                    e.record(self.in_stream)
-                    rnd.events[g] = e
-            else:
-                dst.copy_(seg.data[par * seg.elems + so: par * seg.elems + so + n])
-            rnd.next = i + 1
+            op = _lib.LaneOp(wait_word=seg.word_host(READY), wait_value=seq, dst=dst.data_ptr(),
+                             src=seg.host_ptr(par, so), bytes=dst.numel() * 4)
+            if rnd.timing and i == 0:
+                rnd.ev["i_first"] = self._event(True)
+                ops.append(_lib.LaneOp(wait_word=seg.word_host(READY), wait_value=seq,
+                                       event=rnd.ev["i_first"].cuda_event))
+            if self._group_end[g] == i + 1:
+                op.mark = i + 1
+                if self.gpu:
+                    rnd.events[g] = self._event(rnd.timing)
+                    op.event = rnd.events[g].cuda_event
+            ops.append(op)
+        ack = (r + 1) & 0xFFFFFFFF
+        for src_rank, seg in self.in_seg.items():
+            ops.append(_lib.LaneOp(signal_word=seg.word_dev(ACK) if self.gpu else seg.word_host(ACK),
+                                   signal_value=ack))
+        if rnd.timing:
+            rnd.ev["i1"] = self._event(True)
+            ops.append(_lib.LaneOp(event=rnd.ev["i1"].cuda_event))
+        rnd.ops = (_lib.LaneOp * len(ops))(*ops)  # alive until the round is finished
+        _lib.check("cfa_lane_pump_submit", self._lib.cfa_lane_pump_submit(
+            self._pump, ctypes.cast(rnd.ops, ctypes.c_void_p), len(ops), max(1, int(self.timeout_s * 1e6))))
+
+    def _pump_wait(self, mark: int, rnd: _Round, what: str) -> None:
+        from . import _lib
+        # the pump's own waits time out after timeout_s each; this bound only guards a pump that died
+        rc = self._lib.cfa_lane_pump_wait(self._pump, mark, int((4 * self.timeout_s + 60.0) * 1e6))
+        if rc == _lib.CFA_OK:
+            return
+        msg = (f"round {rnd.r}: the lane failed while {what} "
+               f"({self._lib.cfa_last_error().decode()}); the round's lane rows are invalid")
+        self._error = msg
+        raise LaneTimeout(f"host lane rank {self.rank}: {msg}") if rc == _lib.CFA_E_TIMEOUT else \
+            RuntimeError(f"host lane rank {self.rank}: {msg}")
 
     def pump(self) -> None:
-        """Enqueue the H2D copies of every chunk of the current round that has arrived, in plan
-        order, without waiting (between the interior mixes)."""
-        if self._cur is None or self._cur.done or self._error is not None:
-            return
-        self._advance_to(len(self._in_plan), block=False)
+        """Kept for callers that interleave it with their mixes: the native pump thread enqueues
+        every chunk as it arrives, so there is nothing to do here."""
 
     def advance(self, group: int, rnd: Optional[_Round] = None):
-        """Block (on the host) until every chunk of ``group`` and the groups before it has arrived
-        and its H2D is enqueued; the event after the group's copies (GPU) or None (CPU)."""
+        """Block (on the host; the GIL is released) until the pump has enqueued every chunk of
+        ``group`` and the groups before it; the event after the group's copies (GPU) or None
+        (CPU, where the copies are done)."""
         self.check()
         rnd = rnd or self._cur
         if rnd is None:
             raise RuntimeError("host lane: no round in progress")
         if rnd is self._cur and not rnd.done:
-            self._advance_to(self._group_end.get(group, 0), block=True)
+            self._pump_wait(self._group_end.get(group, 0), rnd, f"waiting for group {group}")
         return rnd.events.get(group)
 
     def finish(self) -> None:
-        """Complete the current round on the host: enqueue every remaining H2D (waiting for its
-        chunk), then the ACK of every incoming segment on the in stream after them."""
+        """Complete the current round on the host: wait until the pump has walked all of it (every
+        H2D and the ACKs enqueued on the in stream)."""
         rnd = self._cur
         if rnd is None:
             return
         self.check()
-        self._advance_to(len(self._in_plan), block=True)
-        ack = (rnd.r + 1) & 0xFFFFFFFF
+        self._pump_wait(-1, rnd, "finishing the round")
         if self.gpu:
-            from . import _lib
-            lib, ish = self._lib, ctypes.c_void_p(self.in_stream.cuda_stream)
-            for src_rank, seg in self.in_seg.items():
-                _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(ACK)), ack, ish))
             if rnd.timing:
-                for k, s in (("o1", self.out_stream), ("i1", self.in_stream)):
-                    rnd.ev[k] = torch.cuda.Event(enable_timing=True)
-                    rnd.ev[k].record(s)
+                rnd.ev["o1"] = torch.cuda.Event(enable_timing=True)
+                rnd.ev["o1"].record(self.out_stream)
                 rnd.ev["groups"] = dict(rnd.events)
             self.last_timing = rnd.ev if rnd.timing else None
-        else:
-            for src_rank, seg in self.in_seg.items():
-                seg.words[ACK] = ack
         rnd.done = True
         self._cur = None
 
@@ -525,9 +548,12 @@ class HostLane:
             stream.wait_stream(self.in_stream)
 
     def close(self) -> None:
-        """Drain the lane's streams, then unpin and drop the segments. A round still in progress
-        is abandoned (its peer's next wait times out)."""
+        """Stop the pump (a round still in progress is abandoned: its peer's next wait times out),
+        drain the lane's streams, then unpin and drop the segments."""
         self._cur = None
+        if self._pump is not None:
+            self._lib.cfa_lane_pump_destroy(self._pump)
+            self._pump = None
         if self.gpu and hasattr(self, "out_stream"):
             self.out_stream.synchronize()
             self.in_stream.synchronize()

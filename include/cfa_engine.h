@@ -264,6 +264,36 @@ CFA_API int cfa_host_register(void* host, size_t bytes);
 CFA_API int cfa_host_unregister(void* host);
 CFA_API int cfa_host_wait_word(const unsigned* word_host, unsigned value, long long timeout_us);
 
+/* The receive side of a host lane as a pump: one native host thread per lane walks a round's
+ * operations in order. Each operation: wait until the host word `wait_word` reaches `wait_value`
+ * (NULL: no wait; the same poll as cfa_host_wait_word, `timeout_us` per wait); copy `bytes` from
+ * `src` to `dst` (0: none); raise `signal_word` to `signal_value` (NULL: none); record `event` (a
+ * hipEvent_t, NULL: none) on the lane's stream; publish `mark` (> 0) as the round's progress.
+ * GPU mode (`host_mode` 0): copies are hipMemcpyAsync on `stream`, signals cfa_stream_signal on it
+ * (`signal_word` a device address), so nothing waits on a GPU queue and the caller's thread does not
+ * wait either until it needs a group's rows. Host mode (1): memcpy and a release store into the host
+ * word (no HIP call; the CPU tests). cfa_lane_pump_submit copies the list and returns at once
+ * (CFA_E_INVALID while the previous round is still in progress); cfa_lane_pump_wait blocks until
+ * `mark` has been published (mark < 0: the whole round) and returns CFA_E_TIMEOUT after
+ * `timeout_us` without it. A wait of the pump that times out ends the round: that error is then
+ * returned by every later wait and submit (sticky). cfa_lane_pump_destroy stops the thread
+ * (interrupting a wait) and frees the pump. One caller thread per pump. */
+typedef struct cfa_lane_op {
+  const unsigned* wait_word;
+  unsigned wait_value;
+  unsigned signal_value;
+  unsigned* signal_word;
+  void* dst;
+  const void* src;
+  size_t bytes;
+  void* event;
+  int mark;
+} cfa_lane_op;
+CFA_API int cfa_lane_pump_create(void** pump, void* stream, int device, int host_mode);
+CFA_API int cfa_lane_pump_submit(void* pump, const cfa_lane_op* ops, int n_ops, long long timeout_us);
+CFA_API int cfa_lane_pump_wait(void* pump, int mark, long long timeout_us);
+CFA_API int cfa_lane_pump_destroy(void* pump);
+
 /* ---------------------------------------------------------------------------------------
  * (a1/a2/a5/a6) Sequential CFA mix of one device with n neighbours.
  *   out[i] = fold_j( w <- w + alphas[j] * (nbrs[j][i] - w) ), w0 = local[i]

@@ -269,3 +269,57 @@ def test_mix_f32_swap_is_stated():
     """Round-4 review: the header claimed cfa_mix_f32 was 'as sketched' while it swaps n and coeff."""
     deps = " ".join(_departures().replace("*", " ").split())
     assert "SWAPPED" in deps and "(out, local, nbrs, n, coeff, P, stream)" in deps
+
+
+def test_lane_pump_host_mode_walks_waits_copies_signals_and_marks():
+    """cfa_lane_pump_* in host mode (no GPU): a round of three operations. The first waits for a word
+    another thread raises later and copies; its mark is published only then (a wait for mark 2 is
+    still pending before); the last raises the ack word. A round whose word never comes ends with
+    CFA_E_TIMEOUT, which is then sticky for waits and submits; destroy interrupts a pending wait."""
+    import ctypes
+    import threading
+    import time
+
+    from federated_amd import _lib
+    lib = _lib.load()
+    words = (ctypes.c_uint * 4)(0, 0, 0, 0)
+    waddr = ctypes.addressof(words)
+    src = (ctypes.c_float * 8)(*range(8))
+    dst = (ctypes.c_float * 8)()
+    pump = ctypes.c_void_p()
+    _lib.check("create", lib.cfa_lane_pump_create(ctypes.byref(pump), None, 0, 1))
+    ops = (_lib.LaneOp * 3)(
+        _lib.LaneOp(wait_word=waddr, wait_value=5, dst=ctypes.addressof(dst), src=ctypes.addressof(src), bytes=16,
+                    mark=1),
+        _lib.LaneOp(wait_word=waddr, wait_value=6, dst=ctypes.addressof(dst) + 16, src=ctypes.addressof(src) + 16,
+                    bytes=16, mark=2),
+        _lib.LaneOp(signal_word=waddr + 4, signal_value=9))
+    _lib.check("submit", lib.cfa_lane_pump_submit(pump, ctypes.cast(ops, ctypes.c_void_p), 3, 5_000_000))
+    assert lib.cfa_lane_pump_submit(pump, ctypes.cast(ops, ctypes.c_void_p), 3, 5_000_000) == _lib.CFA_E_INVALID
+    assert lib.cfa_lane_pump_wait(pump, 1, 50_000) == _lib.CFA_E_TIMEOUT  # word 0 still 0: not yet
+    words[0] = 5
+    assert lib.cfa_lane_pump_wait(pump, 1, 5_000_000) == 0 and list(dst[:4]) == [0.0, 1.0, 2.0, 3.0]
+    assert lib.cfa_lane_pump_wait(pump, 2, 50_000) == _lib.CFA_E_TIMEOUT
+    threading.Timer(0.05, lambda: words.__setitem__(0, 6)).start()
+    assert lib.cfa_lane_pump_wait(pump, -1, 5_000_000) == 0
+    assert list(dst[4:]) == [4.0, 5.0, 6.0, 7.0] and words[1] == 9
+    # a round whose word never comes: the pump's own wait times out after 0.1 s, sticky
+    bad = (_lib.LaneOp * 1)(_lib.LaneOp(wait_word=waddr + 8, wait_value=1, mark=1))
+    _lib.check("submit", lib.cfa_lane_pump_submit(pump, ctypes.cast(bad, ctypes.c_void_p), 1, 100_000))
+    t0 = time.perf_counter()
+    assert lib.cfa_lane_pump_wait(pump, -1, 5_000_000) == _lib.CFA_E_TIMEOUT
+    assert 0.08 < time.perf_counter() - t0 < 3.0 and b"timed out" in lib.cfa_last_error()
+    assert lib.cfa_lane_pump_wait(pump, 1, 1000) == _lib.CFA_E_TIMEOUT
+    assert lib.cfa_lane_pump_submit(pump, ctypes.cast(ops, ctypes.c_void_p), 3, 5_000_000) == _lib.CFA_E_TIMEOUT
+    assert lib.cfa_lane_pump_destroy(pump) == 0
+    # destroy while a wait is pending (60 s timeout): returns promptly
+    p2 = ctypes.c_void_p()
+    _lib.check("create", lib.cfa_lane_pump_create(ctypes.byref(p2), None, 0, 1))
+    _lib.check("submit", lib.cfa_lane_pump_submit(p2, ctypes.cast(bad, ctypes.c_void_p), 1, 60_000_000))
+    time.sleep(0.02)
+    t0 = time.perf_counter()
+    assert lib.cfa_lane_pump_destroy(p2) == 0 and time.perf_counter() - t0 < 2.0
+    with pytest.raises(_lib.CFAError, match="timeout_us must be positive"):
+        _lib.call("cfa_lane_pump_wait", ctypes.c_void_p(1), 1, 0)
+    with pytest.raises(_lib.CFAError, match="null pump"):
+        _lib.call("cfa_lane_pump_submit", None, None, 0, 1)

@@ -8,10 +8,10 @@ streams stalled behind it) and raised the queue count; round 6 removed every wai
 queues (the host lane waits on the host, federated_amd/hostlane.py) and runs at the pool's
 setting. What is left to check is whether ordinary work on one of the rank's streams delays a
 tiny kernel on another: for each pair (A, B) of the rank's stream budget (compute = torch's
-current stream, and federated_amd.streams' comm, lane_out, lane_in), a long piece of work goes on
-A (a 1 GiB H2D copy from pinned memory for the lane streams, ~20 ms; a chain of element-wise
-kernels of about as long for compute / comm), then a tiny kernel on B; B is independent when its
-kernel completes before A's work does. One JSON line.
+current stream, and federated_amd.streams' comm, lane_out, lane_in), each used once first, a long
+piece of work goes on A (a 1 GiB H2D copy from pinned memory for the lane streams, ~20 ms; 60
+element-wise kernels over 1 GiB, ~25 ms, for compute / comm), then a tiny kernel on B; B is
+independent when its kernel completes before A's work does. One JSON line.
 
 Usage (GPU box): [GPU_MAX_HW_QUEUES=n] python tools/probe/hw_queues.py"""
 import json
@@ -32,6 +32,10 @@ def main():
     host = torch.empty(1 << 28, dtype=torch.float32, pin_memory=True)  # 1 GiB
     big = torch.empty(1 << 28, dtype=torch.float32, device=dev)
     x = torch.zeros(1024, device=dev)
+    for s in roles.values():  # every stream used once first (its queue bound, its first launch paid)
+        with torch.cuda.stream(s):
+            x.add_(1.0)
+            big.copy_(host, non_blocking=True)
     torch.cuda.synchronize()
 
     def long_work(s, role):
@@ -39,7 +43,7 @@ def main():
             if role.startswith("lane"):
                 big.copy_(host, non_blocking=True)
             else:
-                for _ in range(12):
+                for _ in range(60):  # ~25 ms of HBM-bound kernels
                     big.mul_(1.0001)
 
     res = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "pairs": []}
