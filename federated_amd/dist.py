@@ -42,14 +42,18 @@ class TorchTransport:
 
     def exchange(self, sends: Sequence[Transfer], recvs: Sequence[Transfer], stream=None) -> None:
         """Grouped exchange. gloo moves host tensors only, so device buffers are staged through
-        host memory (synchronously); with nccl the ops are issued on ``stream``."""
+        host memory, synchronously: the staging copies run on ``stream`` (not on the caller's
+        current stream, whose queued mixes they would otherwise wait for), and ``stream`` is
+        synchronised before the call returns. With nccl the ops are issued on ``stream``."""
         if not sends and not recvs:
             return
         staged = dist.get_backend(self.group) == "gloo"
+        on_dev = staged and stream is not None and any(b.is_cuda for b, _ in list(sends) + list(recvs))
         if staged:
-            if stream is not None and any(b.is_cuda for b, _ in list(sends) + list(recvs)):
+            if on_dev:
                 stream.synchronize()
-            s_bufs = [(b.cpu() if b.is_cuda else b, p) for b, p in sends]
+            with torch.cuda.stream(stream) if on_dev else contextlib.nullcontext():
+                s_bufs = [(b.cpu() if b.is_cuda else b, p) for b, p in sends]
             r_bufs = [(torch.empty(b.shape, dtype=b.dtype) if b.is_cuda else b, p) for b, p in recvs]
         else:
             s_bufs, r_bufs = list(sends), list(recvs)
@@ -59,9 +63,12 @@ class TorchTransport:
             ops += [dist.P2POp(dist.irecv, b, p, group=self.group) for b, p in r_bufs]
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
-        for (dst, _), (src, _) in zip(recvs, r_bufs):
-            if dst is not src:
-                dst.copy_(src)
+        with torch.cuda.stream(stream) if on_dev else contextlib.nullcontext():
+            for (dst, _), (src, _) in zip(recvs, r_bufs):
+                if dst is not src:
+                    dst.copy_(src)
+        if on_dev:
+            stream.synchronize()
 
     def _collective(self, buf: torch.Tensor, stream, fn) -> None:
         """Run ``fn(tensor)`` on ``buf``; gloo moves host tensors only, so a device buffer is

@@ -474,12 +474,17 @@ class RoutedExchange:
         return best[1] if best else None
 
     def run(self, stream=None, stage_done: Optional[Callable[[int], None]] = None,
-            group_done: Optional[Callable[[int], None]] = None, lane_timing: bool = False) -> None:
+            group_done: Optional[Callable[[int], None]] = None, lane_timing: bool = False,
+            before_groups: Optional[Callable[[], None]] = None) -> None:
         """Issue every group in order; ``group_done(g)`` (optional) right after group g is issued
         (the bench's exchange-only timing records an event there). The host lane's copies go first,
-        on its own streams after ``stream``'s earlier work (``lane_timing``: with HIP events)."""
+        on its own streams after ``stream``'s earlier work (``lane_timing``: with HIP events);
+        ``before_groups()`` (optional) runs after them and before the first group (the round's
+        interior mixes, when the transport blocks the host)."""
         if self.lane is not None:
             self._lane_events = self.lane.run(stream, timing=lane_timing)
+        if before_groups is not None:
+            before_groups()
         for g, op in enumerate(self.ops):
             if self.lane is not None:
                 self.lane.pump()

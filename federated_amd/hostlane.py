@@ -256,6 +256,7 @@ class HostLane:
         self._lib = None
         self._pump = None
         self._cur: Optional[_Round] = None
+        self._last_round: Optional[_Round] = None
         self._error: Optional[str] = None
         self.last_timing = None
 
@@ -425,6 +426,9 @@ class HostLane:
                     seq = (r * self._out_n[dst] + k + 1) & 0xFFFFFFFF
                     _lib.check("cfa_stream_signal", lib.cfa_stream_signal(ctypes.c_void_p(seg.word_dev(READY)), seq,
                                                                           osh))
+                if rnd.timing:  # the out stream's work of the round is all enqueued here
+                    rnd.ev["o1"] = torch.cuda.Event(enable_timing=True)
+                    rnd.ev["o1"].record(self.out_stream)
             else:
                 for g, dst, k, so, src in self._out_plan:
                     seg = self.out_seg[dst]
@@ -518,12 +522,11 @@ class HostLane:
         self._pump_wait(-1, rnd, "finishing the round")
         if self.gpu:
             if rnd.timing:
-                rnd.ev["o1"] = torch.cuda.Event(enable_timing=True)
-                rnd.ev["o1"].record(self.out_stream)
                 rnd.ev["groups"] = dict(rnd.events)
             self.last_timing = rnd.ev if rnd.timing else None
         rnd.done = True
         self._cur = None
+        self._last_round = rnd
 
     def timing_ms(self) -> Optional[dict]:
         """After the stream has been synchronised: the last timed round's out-stream and

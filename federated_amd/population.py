@@ -413,10 +413,19 @@ class RingPopulationShard:
             self._mix_set(self.plan.boundary(), cs)
             return
         ms = comm_stream or cs
-        ms.wait_stream(cs)  # models are ready (e.g. written by SGD) before they leave
+        on_gpu = ms.device.type == "cuda" if hasattr(ms, "device") else True
+        # a transport that blocks the host (gloo's host staging) would hold the interior mixes back
+        # until the whole exchange is done: then they are enqueued first, and the exchange waits only
+        # for the models being final (an event before them), not for the mixes
+        early = bool(getattr(self.transport, "host_staged", False)) and on_gpu and ms is not cs
+        if early:
+            ready = torch.cuda.Event()
+            ready.record(cs)
+            ms.wait_event(ready)
+        else:
+            ms.wait_stream(cs)  # models are ready (e.g. written by SGD) before they leave
         sets = self.stage_sets()
         events = {}
-        on_gpu = ms.device.type == "cuda" if hasattr(ms, "device") else True
 
         def landed(stage):
             if on_gpu and ms is not cs:
@@ -424,9 +433,13 @@ class RingPopulationShard:
                 ev.record(ms)
                 events[stage] = ev
 
-        routed.run(ms, landed)
         pump = routed.lane.pump if routed.lane is not None else None
-        self._mix_set(self.interior_order(), cs, timer, pump)
+
+        def interior():
+            self._mix_set(self.interior_order(), cs, timer, pump)
+        routed.run(ms, landed, before_groups=interior if early else None)
+        if not early:
+            interior()
         for stage, devs in sets:
             ev = events.get(stage)
             if ev is not None:
