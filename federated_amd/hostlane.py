@@ -44,6 +44,7 @@ from __future__ import annotations
 import ctypes
 import mmap
 import os
+import weakref
 from typing import Callable, Dict, Hashable, List, Optional, Sequence, Tuple
 
 import torch
@@ -296,6 +297,9 @@ class HostLane:
             (self.device.index if self.device.index is not None else torch.cuda.current_device()) if self.gpu else 0,
             0 if self.gpu else 1))
         self._pump = pump
+        # a lane dropped without close() (an exception, interpreter exit) still stops its pump
+        # thread before the HIP runtime goes away
+        self._pump_finalizer = weakref.finalize(self, self._lib.cfa_lane_pump_destroy, pump)
         self._plan_round()
 
     def unlink(self) -> None:
@@ -555,7 +559,7 @@ class HostLane:
         drain the lane's streams, then unpin and drop the segments."""
         self._cur = None
         if self._pump is not None:
-            self._lib.cfa_lane_pump_destroy(self._pump)
+            self._pump_finalizer()  # cfa_lane_pump_destroy, once
             self._pump = None
         if self.gpu and hasattr(self, "out_stream"):
             self.out_stream.synchronize()
