@@ -324,3 +324,43 @@ def test_two_socket_topology_sheds_cross_pairs():
     nplan, _ = choose_route(world, tr, rates_gbps=naive, lane_chunk_bytes=4 << 20)
     assert plan.predicted_ms(full) <= nplan.predicted_ms(full) + 1e-9
     _check_lane_pairing(plan)
+
+
+def test_numa_helpers_degrade_instead_of_failing():
+    """numa.py: the thread policy on a node this host has is applied and restored; on one it does
+    not have (or with no node) the block still runs and says why; node_of reports a node for a
+    touched page or None. A segment created for a missing node still works."""
+    import mmap as _mmap
+    import ctypes as _ct
+
+    from federated_amd import numa
+    with numa.preferred(0) as why:
+        assert why is None or isinstance(why, str)
+    with numa.preferred(None) as why:
+        assert why == "no NUMA node given"
+    with numa.preferred(1 << 12) as why:  # no such node
+        assert isinstance(why, str) and "set_mempolicy" in why
+    m = _mmap.mmap(-1, 1 << 16)
+    m[0] = 1
+    n = numa.node_of(_ct.addressof(_ct.c_char.from_buffer(m)))
+    assert n is None or n >= 0
+    from federated_amd.hostlane import _Segment
+    path = f"/dev/shm/cfa_lane_test_numa_{os.getpid()}"
+    seg = _Segment(path, 1024, create=True, numa_node=1 << 12)
+    try:
+        assert seg.numa_note and "set_mempolicy" in seg.numa_note
+        seg.data[:4] = torch.arange(4.0)
+        assert seg.data[:4].tolist() == [0.0, 1.0, 2.0, 3.0]
+        assert len(seg.placed_nodes()) >= 1
+    finally:
+        os.unlink(path)
+        seg.close()
+
+
+def test_stream_roles_are_gpu_only_and_named():
+    from federated_amd import streams
+    with pytest.raises(ValueError, match="unknown stream role"):
+        streams.role_stream("compute2", "cuda:0")
+    with pytest.raises(ValueError, match="GPU streams"):
+        streams.role_stream("comm", "cpu")
+    assert isinstance(streams.budget(), dict)
