@@ -1167,15 +1167,16 @@ def main():
                                       lane_token=f"{lane['token']}s{lane['opened']}" if lane["token"] else None,
                                       lane_agree=agree_all, lane_numa_nodes=lane["numa_nodes"])
         lane["opened"] += 1
-        if world > 1 and info.get("lane") is not None:  # every rank's pairs, for config.host_lane
-            pairs = [None] * world
-            dist.all_gather_object(pairs, [dict(p, src=rank) for p in info["lane"]["pairs"]])
-            info["lane"]["pairs_all"] = [p for part in pairs for p in (part or [])]
         if world > 1 and "route_digest" in info:  # every rank must run the same schedule
             digests = [None] * world
             dist.all_gather_object(digests, info["route_digest"])
             if len(set(digests)) != 1:
                 raise RuntimeError("route plans differ across ranks")
+        if world > 1 and (info.get("route") or {}).get("lane"):  # every rank's pairs, for config.host_lane
+            pairs = [None] * world
+            mine = (info.get("lane") or {}).get("pairs") or []
+            dist.all_gather_object(pairs, [dict(p, src=rank) for p in mine])
+            info["lane"]["pairs_all"] = [p for part in pairs for p in (part or [])]
         seed_shard(shard, info, P)
         return shard, info
 

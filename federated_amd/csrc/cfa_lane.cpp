@@ -23,6 +23,8 @@
 // submit returns it. Destroy stops the thread, interrupting a wait.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <condition_variable>
@@ -65,7 +67,7 @@ struct Pump {
   std::vector<cfa_lane_op> ops;  // the round being walked
   long long timeout_us = 0;
   bool job = false;       // a round has been submitted and is not finished
-  bool stop = false;
+  std::atomic<bool> stop{false};  // read by the polling loop without the lock
   int progress = 0;       // highest mark published in the current round
   int error = CFA_OK;     // sticky
   std::string message;
@@ -79,7 +81,7 @@ struct Pump {
     for (unsigned i = 1;; ++i) {
       if (reached(w, value)) return CFA_OK;
       if ((i & 63) == 0) {
-        if (__atomic_load_n(&stop, __ATOMIC_RELAXED)) return 1;
+        if (stop.load(std::memory_order_relaxed)) return 1;
         const auto dt = std::chrono::steady_clock::now() - t0;
         if (dt > limit) break;
         if (dt > spin) std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -202,11 +204,20 @@ extern "C" int cfa_lane_pump_wait(void* pump, int mark, long long timeout_us) {
   if (timeout_us <= 0) return lfail(CFA_E_INVALID, "timeout_us must be positive (got %lld)", timeout_us);
   const int want = mark < 0 ? INT_MAX : mark;
   std::unique_lock<std::mutex> lk(p->mu);
-  const bool ok = p->cv.wait_for(lk, std::chrono::microseconds(timeout_us),
-                                 [&] { return p->error != CFA_OK || p->progress >= want; });
+  auto done = [&] { return p->error != CFA_OK || p->progress >= want; };
+  // The deadline is on the steady clock; the waits are system-clock slices of at most 100 ms
+  // (pthread_cond_timedwait, which ThreadSanitizer models; a clock jump costs one slice at most).
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+  while (!done()) {
+    const auto now = std::chrono::steady_clock::now();
+    if (now >= deadline) break;
+    const auto slice = std::min<std::chrono::steady_clock::duration>(deadline - now, std::chrono::milliseconds(100));
+    p->cv.wait_until(lk, std::chrono::system_clock::now() +
+                             std::chrono::duration_cast<std::chrono::system_clock::duration>(slice));
+  }
   if (p->error != CFA_OK) return lfail(p->error, "lane pump: %s", p->message.c_str());
-  if (!ok) return lfail(CFA_E_TIMEOUT, "lane pump: mark %d not reached after %lld us (at %d)", mark, timeout_us,
-                        p->progress);
+  if (!done()) return lfail(CFA_E_TIMEOUT, "lane pump: mark %d not reached after %lld us (at %d)", mark, timeout_us,
+                            p->progress);
   return CFA_OK;
 }
 
@@ -215,7 +226,7 @@ extern "C" int cfa_lane_pump_destroy(void* pump) {
   if (!p) return CFA_OK;
   {
     std::lock_guard<std::mutex> g(p->mu);
-    p->stop = true;
+    p->stop.store(true);
     p->cv.notify_all();
   }
   if (p->worker.joinable()) p->worker.join();
