@@ -35,7 +35,7 @@ set -u
 TAG=${1:?tag}; shift
 OUT=gpurun_out; mkdir -p "$OUT"; cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic --no-e2e"
+BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic --no-e2e --placement-leg 0"  # the headline alone
 OKRC=" 0 "
 step() {
   local name=$1 t=$2; shift 2
