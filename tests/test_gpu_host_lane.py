@@ -172,3 +172,93 @@ def test_late_peer_does_not_hold_the_compute_stream(gpu):
                 p.kill()
     assert res[0]["compute_done_while_peer_late"] and not res[0]["peer_arrived_by_then"]
     assert res[0]["rows_ok"] and res[1]["rows_ok"]
+
+
+def _fuzz_worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from federated_amd.dist import TorchTransport
+        from federated_amd.engine import get_engine
+        from federated_amd.halo import LANE_IN, LANE_OUT
+        from federated_amd.hostlane import new_token
+        from federated_amd.linkprobe import agree_gloo
+        from federated_amd.population import make_ring_shard
+        from federated_amd.streams import role_stream
+        eng = get_engine(0)
+        outs = []
+        for ci, (D, h, P, chunk, lane_rate, rounds) in enumerate(cases):
+            tok = [new_token() if rank == 0 else None]
+            dist.broadcast_object_list(tok, src=0)
+            rates = {(a, b): 50.0 for a in range(world) for b in range(world) if a != b}
+            rates.update({(a, LANE_OUT): lane_rate for a in range(world)})
+            rates.update({(LANE_IN, a): lane_rate for a in range(world)})
+            shard, info = make_ring_shard(rank, world, D, h, h, P, torch.device("cuda", 0), TorchTransport(), eng,
+                                          link_rates=rates, lane_token=tok[0], lane_agree=agree_gloo,
+                                          lane_chunk_elems=chunk)
+            for i in range(shard.plan.L):
+                g = shard.plan.first + i
+                shard.models[i].copy_(torch.randn(P, generator=torch.Generator().manual_seed(900 + 17 * g + ci)))
+            cs = torch.cuda.current_stream()
+            for _ in range(rounds):
+                shard.round(cs, role_stream("comm"))
+                shard.models.copy_(shard.mixed)
+            torch.cuda.synchronize()
+            outs.append(({shard.plan.first + i: shard.models[i].cpu().numpy() for i in range(shard.plan.L)},
+                         bool(info["route"]["lane"])))
+            shard.close()
+        q.put((rank, outs))
+    except Exception as exc:
+        q.put((rank, f"{type(exc).__name__}: {exc}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_lane_random_populations_match_the_oracle(gpu):
+    """Four random ring populations (window 1-4 per side, odd bucket lengths, chunk sizes from one
+    aligned piece to many per row, lane rates from a sliver of the halo to most of it), two
+    processes on the GPU, three rounds with the mixed models fed back, every device bit for bit
+    against the unsharded oracle trajectory: the lane's host-side pump under the HIP kernels."""
+    import random
+
+    import torch.multiprocessing as mp
+    from federated_amd.population import RingShardPlan
+    from oracle.cfa_oracle import sequential_mix
+    rng = random.Random(20261018)
+    world, cases = 2, []
+    for _ in range(4):
+        h = rng.randint(1, 4)
+        cases.append((world * rng.randint(2 * h, 2 * h + 2), h, rng.randint(2_000, 60_000) * 2 + 1,
+                      64 * rng.randint(1, 200), rng.choice([20.0, 50.0, 200.0]), 3))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 34900 + (os.getpid() % 997)
+    procs = [ctx.Process(target=_fuzz_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in procs:
+            rank, out = q.get(timeout=100)
+            assert not isinstance(out, str), f"rank {rank}: {out}"
+            got[rank] = out
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    used = 0
+    for ci, (D, h, P, chunk, lane_rate, rounds) in enumerate(cases):
+        ring = RingShardPlan(0, 1, D, h)
+        cur = [torch.randn(P, generator=torch.Generator().manual_seed(900 + 17 * g + ci)).numpy() for g in range(D)]
+        alphas = [1.0 / (2 * h + 1)] * (2 * h)
+        for _ in range(rounds):
+            cur = [sequential_mix(cur[g], [cur[j] for j in ring.neighbours(g)], alphas) for g in range(D)]
+        mine = {**got[0][ci][0], **got[1][ci][0]}
+        used += got[0][ci][1]
+        for g in range(D):
+            assert np.array_equal(mine[g], cur[g]), (ci, g)
+    assert used >= 1

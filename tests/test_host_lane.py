@@ -364,3 +364,72 @@ def test_stream_roles_are_gpu_only_and_named():
     with pytest.raises(ValueError, match="GPU streams"):
         streams.role_stream("comm", "cpu")
     assert isinstance(streams.budget(), dict)
+
+
+def _fuzz_worker(rank, world, port, cases, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from federated_amd.dist import TorchTransport
+        from federated_amd.hostlane import new_token
+        from federated_amd.linkprobe import agree_gloo
+        from federated_amd.population import make_ring_shard
+        results = []
+        for ci, (D, h, P, chunk, lane_rate, rounds) in enumerate(cases):
+            tok = [new_token() if rank == 0 else None]
+            dist.broadcast_object_list(tok, src=0)
+            rates = _rates(world, 50.0, lane_rate)
+            shard, info = make_ring_shard(rank, world, D, h, h, P, "cpu", TorchTransport(), None, relay=True,
+                                          link_rates=rates, lane_token=tok[0], lane_agree=agree_gloo,
+                                          lane_chunk_elems=chunk)
+            ok = True
+            for r in range(rounds):
+                for i in range(shard.plan.L):
+                    g = shard.plan.first + i
+                    shard.models[i] = torch.randn(P, generator=torch.Generator().manual_seed(31 * g + 7 * r + ci))
+                shard.exchange()
+                for i in shard.plan.boundary():
+                    g = shard.plan.first + i
+                    for src, j in zip(shard.sources(i), shard.plan.neighbours(g)):
+                        want = torch.randn(P, generator=torch.Generator().manual_seed(31 * j + 7 * r + ci))
+                        ok &= torch.equal(src, want)
+            results.append((ci, bool(ok), bool(info["route"]["lane"]), info["route"]["lane_elems"]))
+            shard.close()
+        q.put((rank, results))
+    except Exception as exc:
+        q.put((rank, f"{type(exc).__name__}: {exc}"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_lane_random_plans_gloo(world):
+    """Random ring populations (devices, window, odd bucket lengths, chunk sizes from one aligned
+    piece to several pieces per row, lane rates that give the lane anything from a sliver to most
+    of the halo), three rounds each, with fresh models every round: every halo row any boundary
+    device reads equals its owner's row of that round, on every rank."""
+    import random
+    rng = random.Random(4242 + world)
+    cases = []
+    for _ in range(5):
+        h = rng.randint(1, 3)
+        D = world * rng.randint(2 * h, 2 * h + 3)
+        cases.append((D, h, rng.randint(300, 4000) * 3 + 1, 64 * rng.randint(1, 40), rng.choice([5.0, 25.0, 50.0, 200.0]),
+                      3))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35900 + (os.getpid() % 997) + world * 13
+    procs = [ctx.Process(target=_fuzz_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, out = q.get(timeout=240)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+    for r, out in res.items():
+        assert not isinstance(out, str), f"rank {r}: {out}"
+        assert all(ok for _, ok, _, _ in out), (r, out)
+    assert any(used for _, _, used, _ in res[0])  # the lane carried pieces in some of the plans
