@@ -194,10 +194,10 @@ class _Round:
 
 
 class LaneGate:
-    """What ``HostLane.run`` hands out per group: ``wait(stream)`` makes ``stream`` wait for the
-    group's lane pieces (and every earlier group's), pumping the lane on the host until they have
-    been enqueued; it is what ``torch.cuda.Stream.wait_event`` calls, so a gate stands where an
-    event would."""
+    """What ``HostLane.run`` hands out per group: ``wait(stream)`` blocks on the host (GIL
+    released) until the lane's pump thread has enqueued the group's lane pieces (and every
+    earlier group's), then makes ``stream`` wait on the event after their copies; it is what
+    ``torch.cuda.Stream.wait_event`` calls, so a gate stands where an event would."""
 
     def __init__(self, lane: "HostLane", rnd: _Round, group: int):
         self.lane, self.rnd, self.group = lane, rnd, group
@@ -212,9 +212,10 @@ class HostLane:
     """The host-lane messages of one rank, bound to its buffers and the pair segments.
 
     Build with ``HostLane.open`` (collective: every rank of the plan calls it). ``run(stream)``
-    starts one round after ``stream``'s earlier work and returns {group index: LaneGate};
-    ``pump()`` / a gate's ``wait`` / ``finish()`` enqueue the receiving side as its chunks arrive
-    (see the module docstring). On CPU tensors the copies happen at once, in the same calls."""
+    starts one round after ``stream``'s earlier work and returns {group index: LaneGate}; the
+    lane's pump thread enqueues the receiving side as its chunks arrive, and a gate's ``wait`` or
+    ``finish()`` blocks until it has (see the module docstring). On CPU tensors the pump copies
+    with memcpy (host mode)."""
 
     def __init__(self, rank: int, sends: Sequence[Message], recvs: Sequence[Message],
                  buffers: Callable[[Hashable], torch.Tensor], device, token: str,
