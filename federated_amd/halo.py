@@ -426,8 +426,9 @@ class RoutedExchange:
     ``stream`` and calls ``stage_done(stage)`` right after the group that completes each stage,
     so the caller can record an event there and start that stage's boundary mixes. A plan with
     host-lane messages needs ``lane`` (a ``hostlane.HostLane`` opened on the same plan): ``run``
-    issues its copies first, on the lane's own streams, and ``lane_event(stage)`` is the event
-    after which the lane's pieces of that stage (and every earlier one) have landed."""
+    starts its round first (the D2H side on the lane's own stream, the receive side on its pump
+    thread), and ``lane_event(stage)`` is the gate a stream waits on for the lane's pieces of that
+    stage (and every earlier one); ``finish_lane`` completes the lane's round on the host."""
 
     def __init__(self, plan: RoutePlan, rank: int, buffers: Callable[[Hashable], "object"], transport,
                  device=None, dtype=None, relay=None, lane=None):
