@@ -227,6 +227,8 @@ class HostLane:
         may need, so it fails where the headline would); both ends must pass the same value."""
         self.rank, self.token = int(rank), str(token)
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:  # "cuda" means the current GPU
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.gpu = self.device.type == "cuda"
         self.chunk_elems = max(ALIGN, int(chunk_elems) // ALIGN * ALIGN)
         self.timeout_s = float(timeout_s)
@@ -295,8 +297,7 @@ class HostLane:
         pump = ctypes.c_void_p()
         _lib.check("cfa_lane_pump_create", self._lib.cfa_lane_pump_create(
             ctypes.byref(pump), ctypes.c_void_p(self.in_stream.cuda_stream if self.gpu else 0),
-            (self.device.index if self.device.index is not None else torch.cuda.current_device()) if self.gpu else 0,
-            0 if self.gpu else 1))
+            self.device.index if self.gpu else 0, 0 if self.gpu else 1))
         self._pump = pump
         # a lane dropped without close() (an exception, interpreter exit) still stops its pump
         # thread before the HIP runtime goes away
