@@ -8,7 +8,8 @@ one process on the one GPU (tests/loopback.py: device-to-device copies with cfa_
 pairing, not host-staged), each with its own host lane (real shared-memory segments, pinned, one
 pump thread per lane, its own lane streams), the route planned on rates that put part of the halo
 on the lane; several rounds with the mixed models fed back, every device bit for bit against the
-unsharded oracle trajectory. Worlds 2 (one pair, both halos) and 4 (relays and the lane together).
+unsharded oracle trajectory. Worlds 2 (one pair, both halos), 4 and 8 (the bench's N = 8 plan: relays and
+the lane together).
 """
 import threading
 
@@ -38,7 +39,7 @@ class _Agree:
         return agree
 
 
-@pytest.mark.parametrize("world,D,P", [(2, 32, 300_037), (4, 64, 200_003)])
+@pytest.mark.parametrize("world,D,P", [(2, 32, 300_037), (4, 64, 200_003), (8, 128, 100_003)])
 def test_lane_exchange_first_round_matches_the_oracle(gpu, monkeypatch, world, D, P):
     from loopback import LoopbackHub, run_ranks
     from federated_amd import hostlane, streams
