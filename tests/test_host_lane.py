@@ -433,3 +433,34 @@ def test_host_lane_random_plans_gloo(world):
         assert not isinstance(out, str), f"rank {r}: {out}"
         assert all(ok for _, ok, _, _ in out), (r, out)
     assert any(used for _, _, used, _ in res[0])  # the lane carried pieces in some of the plans
+
+
+def test_pair_links_in_plan_loads_and_prices():
+    """A priced lane pair loads its own pseudo-link beside the two rank links, in the plan's link
+    loads and its predicted group time; unpriced pairs do not. lane_pair_rates leaves the rates
+    alone with missing or partial node information."""
+    from federated_amd.halo import lane_pair, lane_pair_dst, priced_pairs
+    from federated_amd.linkprobe import lane_pair_rates
+    assert lane_pair_dst(lane_pair(5)) == 5 and lane_pair_dst(LANE_OUT) is None and lane_pair_dst(LANE_IN) is None
+    tr = ring_transfers(2, 16, 4, 4, 100_000)
+    rates = _rates(2, 50.0, 50.0)
+    rates[(0, lane_pair(1))] = 10.0  # only 0 -> 1 crosses sockets
+    assert priced_pairs(rates) == {(0, 1)}
+    plan = RoutePlan(2, tr, lane=True, lane_pairs=priced_pairs(rates))
+    assert plan.lane
+    loads = {}
+    for g in range(len(plan.groups)):
+        for l, n in plan.group_link_elems(g).items():
+            loads[l] = loads.get(l, 0) + n
+    per = plan.lane_pair_elems()
+    assert loads.get((0, lane_pair(1)), 0) == per.get((0, 1), 0) > 0
+    assert (1, lane_pair(0)) not in loads
+    # the slow pair link sets the price of groups that carry 0 -> 1 lane pieces
+    fast = plan.predicted_ms({k: v for k, v in rates.items() if k != (0, lane_pair(1))})
+    assert plan.predicted_ms(rates) > fast
+    probe = {"rates": {(0, LANE_OUT): 50.0, (1, LANE_OUT): 20.0, (LANE_IN, 0): 50.0, (LANE_IN, 1): 50.0},
+             "out_GBps": [50.0, 20.0], "pairs": [[0, 1], [1, 0]]}
+    assert lane_pair_rates(probe, [0, None]) == probe["rates"]  # a node unknown: unchanged
+    assert lane_pair_rates(probe, [0]) == probe["rates"]        # too short: unchanged
+    both_cross = lane_pair_rates(probe, [0, 1])                  # no same-node probe pair: ranks keep theirs
+    assert both_cross[(1, LANE_OUT)] == 20.0 and both_cross[(0, lane_pair(1))] == 20.0
