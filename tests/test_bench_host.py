@@ -414,3 +414,17 @@ def test_lane_fallback_without_a_lane_reports_the_error():
     lane, probe = {"error": None}, {"plan_rates": {(0, 1): 50.0, (1, 0): 50.0}}
     res, err = bench.headline_with_lane_fallback(measure, lambda ok: ok, lane, probe)
     assert res is None and "rccl says no" in err and len(calls) == 1 and lane["error"] is None
+
+
+def test_headline_is_plain_allocation_and_the_calibrated_placement_is_a_leg(monkeypatch):
+    """Round-5 review item 4: `value` is measured on plain allocations (what users get); the
+    placement-calibrated rounds are the N = 1 leg `legs.placement_calibrated` (asserted on the GPU
+    line by tests/test_gpu_bench_contract.py), never the headline."""
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert a.placement_candidates == 1 and a.placement_leg == 4
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'legs_n1["placement_calibrated"]' in src and 'result["legs"] = legs_n1' in src
+    # the profiling runs time the headline alone
+    assert "--placement-leg 0" in open(os.path.join(ROOT, "tools", "gpu_session.sh")).read()
