@@ -20,6 +20,8 @@ import torch
 
 from ..engine import get_engine
 
+_STREAMS: dict = {}
+
 
 def same_pad(L: int, k: int, s: int):
     """TF SAME padding: out = ceil(L / s), total = max((out - 1) s + k - L, 0), left = total // 2."""
@@ -138,7 +140,9 @@ def gradients_batched(ml_model: int, x, y, models: Sequence, stride: int = 1, de
         if plans is None:
             plans = hm._tls.grad_plans = {}
     else:
-        st = torch.cuda.Stream(eng.device)
+        st = _STREAMS.get(eng.device)
+        if st is None:  # one stream per device for calls without a HostMixer, not one per call
+            st = _STREAMS[eng.device] = torch.cuda.Stream(eng.device)
         plans = {}
     plan = plans.get(key)
     if plan is None:
