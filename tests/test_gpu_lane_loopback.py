@@ -9,7 +9,7 @@ pairing, not host-staged), each with its own host lane (real shared-memory segme
 pump thread per lane, its own lane streams), the route planned on rates that put part of the halo
 on the lane; several rounds with the mixed models fed back, every device bit for bit against the
 unsharded oracle trajectory. Worlds 2 (one pair, both halos), 4 and 8 (the bench's N = 8 plan: relays and
-the lane together).
+the lane together), and the hybrid partition at world 4 (2 device blocks x 2 element slices).
 """
 import threading
 
@@ -39,8 +39,9 @@ class _Agree:
         return agree
 
 
-@pytest.mark.parametrize("world,D,P", [(2, 32, 300_037), (4, 64, 200_003), (8, 128, 100_003)])
-def test_lane_exchange_first_round_matches_the_oracle(gpu, monkeypatch, world, D, P):
+@pytest.mark.parametrize("world,D,P,partition", [(2, 32, 300_037, "devices"), (4, 64, 200_003, "devices"),
+                                                 (8, 128, 100_003, "devices"), (4, 32, 200_003, "hybrid")])
+def test_lane_exchange_first_round_matches_the_oracle(gpu, monkeypatch, world, D, P, partition):
     from loopback import LoopbackHub, run_ranks
     from federated_amd import hostlane, streams
     from federated_amd.halo import LANE_IN, LANE_OUT
@@ -68,18 +69,21 @@ def test_lane_exchange_first_round_matches_the_oracle(gpu, monkeypatch, world, D
     def rank_fn(rank, transport):
         assert not getattr(transport, "host_staged", False)  # the exchange-first order
         shard, info = make_ring_shard(rank, world, D, h, h, P, torch.device("cuda"), transport, gpu,
+                                      partition=partition, dev_groups=2 if partition == "hybrid" else None,
                                       link_rates=rates, lane_token=token, lane_agree=agree.of(rank),
                                       lane_chunk_elems=1 << 14)
+        lo, hi = info["slice"]
         try:
             cs, ms = torch.cuda.Stream(), torch.cuda.Stream()
             with torch.cuda.stream(cs):
                 for i in range(shard.plan.L):
-                    shard.models[i].copy_(torch.from_numpy(full[shard.plan.first + i]))
+                    shard.models[i].copy_(torch.from_numpy(full[shard.plan.first + i][lo:hi]))
                 for _ in range(rounds):
                     shard.round(cs, ms)
                     shard.models.copy_(shard.mixed)
             cs.synchronize()
-            return shard.plan.first, shard.models.cpu().numpy(), info["route"]["lane"], info["route"]["lane_elems"]
+            return (shard.plan.first, shard.models.cpu().numpy(), info["route"]["lane"], info["route"]["lane_elems"],
+                    (lo, hi))
         finally:
             shard.close()
 
@@ -93,6 +97,6 @@ def test_lane_exchange_first_round_matches_the_oracle(gpu, monkeypatch, world, D
     for _ in range(rounds):
         cur = [sequential_mix(cur[d], [cur[(d + o) % D] for o in offs], [1.0 / (2 * h + 1)] * (2 * h))
                for d in range(D)]
-    for first, block, _, _ in res:
+    for first, block, _, _, (lo, hi) in res:  # hybrid: each rank holds an element slice of its block
         for i in range(block.shape[0]):
-            assert np.array_equal(block[i], cur[first + i]), first + i
+            assert np.array_equal(block[i], cur[first + i][lo:hi]), first + i
